@@ -1,0 +1,204 @@
+"""bench.py — Mpaths/s of the wavefront path tracer (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): mitsuba_synth (stand-in for the absent
+mitsuba.obj), 1024 x 1024, 64 spp, 8 ray casts per path.  One step = one
+full render of that image: every rank renders its interleaved row-group
+tile, the fp32 tiles are gathered to rank 0 over RCCL and assembled.  With N
+GPUs the same image is split N ways (strong scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints one JSON line (rank 0) with the metric, the isect kernel's roofline
+(HIP events on the render stream) and the CPU-oracle baseline timed on this
+host (N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ISECT_BYTES_PER_CAST = 44      # ray 24 B + meta 4 B in, hit 16 B out
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--height", type=int, default=1024)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--scene", default="mitsuba_synth")
+    ap.add_argument("--rows-per-group", type=int, default=8)
+    ap.add_argument("--ppp", type=int, default=0, help="paths per pixel in flight (0 = auto)")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save", default="", help="write the rank-0 image (.npy) here")
+    return ap.parse_args()
+
+
+def cpu_baseline(mesh, args, threads):
+    """Oracle (oracle/, a C restatement of main.cpp:354-446) on a bounded row
+    sample of the same workload, on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    sc = O.OracleScene(mesh)
+    p = O.reference_params(args.width, args.height, args.spp, args.depth)
+    stride = 64
+    rows = np.arange(0, args.height, stride, dtype=np.int32)[:4]
+    t0 = time.perf_counter()
+    sc.render(p, rows=rows, nthreads=threads)
+    dt = time.perf_counter() - t0
+    # scale the sample to ~cpu_baseline_seconds of work, rows spread over the image
+    want = int(max(1, min(args.height, len(rows) * args.cpu_baseline_seconds / max(dt, 1e-3))))
+    stride = max(1, args.height // want)
+    rows = np.arange(0, args.height, stride, dtype=np.int32)[:want]
+    t0 = time.perf_counter()
+    _, casts = sc.render(p, rows=rows, nthreads=threads)
+    dt = time.perf_counter() - t0
+    paths = rows.size * args.width * args.spp
+    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"{rows.size} of {args.height} rows (every {stride}th) x {args.width} px x {args.spp} spp, "
+                      f"depth {args.depth}: {paths} paths, {casts} casts in {dt:.2f} s "
+                      f"(oracle: C restatement, median-split BVH, {threads} threads)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import sptamd
+    from sptamd import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # scene: generated stand-in, loaded through the OBJ reader like main.cpp:365
+    obj = scenes.scene_obj(args.scene) if rank == 0 or world == 1 else None
+    if world > 1:
+        dist.barrier()
+        obj = scenes.scene_obj(args.scene)
+    scene = sptamd.Scene()
+    scene.add_triangle_mesh(obj)
+    scene.commit(local)
+    sstats = scene.backend.stats
+
+    W, H = args.width, args.height
+    R = args.rows_per_group
+    params = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
+                                paths_per_pixel=args.ppp, timing=True)
+    rows_all = [sptamd.tile_rows(H, r, world, R) for r in range(world)]
+    max_rows = max(len(r) for r in rows_all)
+    dev = torch.device("cuda", local)
+    tile = torch.zeros((3, max_rows, W), dtype=torch.float32, device=dev)
+    my_rows = len(rows_all[rank])
+    gather_list = [torch.empty_like(tile) for _ in range(world)] if rank == 0 and world > 1 else None
+    image = torch.empty((3, H, W), dtype=torch.float32, device=dev) if rank == 0 else None
+    row_index = [torch.as_tensor(r, device=dev) for r in rows_all] if rank == 0 else None
+    stream = torch.cuda.current_stream()
+
+    def step():
+        _, st = scene.render(params, film=tile, stream=stream)
+        if world > 1:
+            dist.gather(tile, gather_list, dst=0)
+            if rank == 0:
+                for r in range(world):
+                    image[:, row_index[r], :] = gather_list[r][:, :len(rows_all[r]), :]
+        else:
+            image.copy_(tile[:, :H, :])
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
+           "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0}
+    st = {}
+    for _ in range(args.steps):
+        st = step()
+        for k in agg:
+            agg[k] += st[k]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([agg["ray_casts"], agg["isect_ms"], agg["iterations"]], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        agg_casts_all = float(tot[0].item())
+    else:
+        agg_casts_all = float(agg["ray_casts"])
+
+    paths = W * H * args.spp * args.steps
+    value = paths / elapsed / 1e6
+    if rank == 0:
+        # isect roofline: algorithmic bytes per launch / average launch time (rank 0's tile)
+        launches = max(agg["iterations"], 1)
+        avg_ms = agg["isect_ms"] / launches
+        bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        rec = {
+            "metric": "Mpaths/sec (pixels x spp / s), mitsuba.obj-standin 1024^2 x 64spp, depth 8",
+            "value": round(value, 3),
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (mitsuba_synth stand-in generated in-run; reference asset absent)",
+            "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}",
+                       "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
+                       "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "isect_queue_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "algorithmic_bytes_per_launch": round(bytes_per_launch),
+                         "grays_per_s": round(agg["ray_casts"] / (agg["isect_ms"] * 1e-3) / 1e9, 4)
+                         if agg["isect_ms"] else None},
+            "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
+                                   ("isect_ms", "shade_ms", "camera_ms", "resolve_ms")},
+            "bvh": {k: sstats[k] for k in ("nodes", "max_depth", "build_ms", "sah_cost")},
+        }
+        if args.save:
+            np.save(args.save, image.cpu().numpy())
+        if world == 1 and not args.no_cpu_baseline:
+            mesh = scenes.load_obj(obj)
+            rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,200 @@
+/*
+ * spt.h — C ABI of the MI355X-native wavefront path tracer (the drop-in
+ * boundary for the reference's OptiX backend + Enoki bounce loop).
+ *
+ * Plain C: pointers, sizes, status codes.  Device buffers are HIP device
+ * pointers (hipMalloc / torch CUDA tensors); `stream` is a hipStream_t passed
+ * as void* (NULL = default stream).  Citations are reference paths:lines
+ * (jamornsriwasansak/smallpt-enoki-optix).
+ *
+ * Error behaviour: every call returns SPT_OK (0) or an error code and stores a
+ * message for spt_last_error() (the reference throws std::runtime_error from
+ * OPTIX_CHECK / CUDA_CHECK, optix_backend.h:25-66; the C++ host wrapper in
+ * smallpt-enoki-optix_amd/csrc/spt.hpp rethrows with that convention).
+ */
+#ifndef SPT_H
+#define SPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t spt_status;
+enum {
+    SPT_OK = 0,
+    SPT_ERR_INVALID = 1,   /* bad argument / shape */
+    SPT_ERR_HIP = 2,       /* HIP runtime failure */
+    SPT_ERR_NO_DEVICE = 3, /* no GPU visible */
+    SPT_ERR_OOM = 4,       /* device allocation failed */
+    SPT_ERR_IO = 5,        /* file could not be read / written */
+    SPT_ERR_LIMIT = 6      /* size beyond a documented limit */
+};
+
+typedef struct spt_scene_t* spt_scene;
+
+/* SoA ray planes — optixdata.h:13-20 (Params::m_ray_*), ray.h:28-31. */
+typedef struct spt_rays {
+    const float* ox; const float* oy; const float* oz;
+    const float* dx; const float* dy; const float* dz;
+    const float* tmin; const float* tmax;
+} spt_rays;
+
+/* SoA hit planes — optixdata.h:23-26 (m_result_tri_id / _t / _barycentric_u / _v). */
+typedef struct spt_hits {
+    int32_t* tri_id; float* t; float* u; float* v;
+} spt_hits;
+
+/* Reconstructed surface — optix_backend.h:99-134 (TriangleHitInfo) plus the
+ * material id gathered by Scene::intersect (main.cpp:325).  Each pointer may be
+ * NULL to skip that output.  Planar SoA, n elements per plane. */
+typedef struct spt_hit_info {
+    float* px; float* py; float* pz;          /* position o + t d          (:469)     */
+    float* gnx; float* gny; float* gnz;       /* geometric normal          (:472-476) */
+    float* snx; float* sny; float* snz;       /* shading normal, un-normalised (:483-484) */
+    float* tcu; float* tcv;                   /* texcoord                  (:479-480) */
+    int32_t* mat_id;                          /* material id (obj id + 1)  (main.cpp:325) */
+} spt_hit_info;
+
+/* ThinlensCamera — pinhole.h:9-16, constructed at main.cpp:383. */
+typedef struct spt_camera {
+    float look_from[3];
+    float look_at[3];
+    float up[3];
+    float lens_radius;
+    float focal_dist;
+    float fov_y;        /* radians */
+    float film_size_y;  /* 0.035 default (pinhole.h:11) */
+} spt_camera;
+
+enum {
+    SPT_RNG_Y_FIRST = 0,  /* Real2C(a, b) with b drawn first (MSVC/GCC order) */
+    SPT_RNG_X_FIRST = 1
+};
+
+enum {
+    SPT_FLAG_TIMING = 1u  /* record HIP events around every isect/shade launch */
+};
+
+/* The render loop of main.cpp:354-429 plus the tile/wavefront knobs. */
+typedef struct spt_render_params {
+    uint32_t width, height;     /* main.cpp:357-358 */
+    uint32_t spp;               /* main.cpp:360 */
+    uint32_t max_depth;         /* ray casts per path, main.cpp:361 (num_bounces) */
+    spt_camera camera;
+    /* Interleaved row-group tiling: global row r belongs to tile
+     * (r / rows_per_group) % tile_count.  tile_count = 1 renders the image. */
+    uint32_t tile_index, tile_count, rows_per_group;
+    uint32_t paths_per_pixel;   /* samples of one pixel in flight (0 = auto) */
+    uint32_t rr_start_depth;    /* Russian roulette from this cast on (>= max_depth: off) */
+    uint32_t rng_order;         /* SPT_RNG_* */
+    uint64_t rng_initstate;     /* PCG32_DEFAULT_STATE 0x853c49e6748fea9b (main.cpp:376) */
+    float env[3];               /* sky radiance on miss, 1 in the reference (main.cpp:407) */
+    uint32_t flags;             /* SPT_FLAG_* */
+} spt_render_params;
+
+typedef struct spt_render_stats {
+    uint64_t paths;             /* pixels x spp rendered by this call */
+    uint64_t ray_casts;         /* closest/any-hit queries traced */
+    uint64_t continuations;     /* paths that bounced into a next cast */
+    uint64_t regenerations;     /* camera rays started in-loop (path regeneration) */
+    uint64_t iterations;        /* isect+shade launch pairs */
+    uint32_t paths_in_flight;   /* wavefront capacity (tile pixels x paths_per_pixel) */
+    uint32_t tile_rows;
+    double isect_ms, shade_ms, camera_ms, resolve_ms; /* SPT_FLAG_TIMING only */
+    double total_ms;            /* host wall time of the call (includes final sync) */
+} spt_render_stats;
+
+typedef struct spt_scene_stats {
+    uint64_t ntri, nodes, leaves;
+    uint32_t max_depth;         /* BVH depth (sets the LDS stack depth) */
+    uint32_t max_leaf;
+    uint64_t device_bytes;
+    double build_ms;            /* host SAH build */
+    double sah_cost;
+} spt_scene_stats;
+
+/* Host-side mesh (main.cpp:133-251 load_meshes; flat arrays like
+ * set_triangles_soup's inputs).  Owned by the library; free with spt_mesh_free. */
+typedef struct spt_mesh {
+    int32_t* pos_tri; float* pos; uint64_t nvert, ntri;
+    int32_t* nrm_tri; float* nrm; uint64_t nnrm;
+    int32_t* tc_tri; float* tc; uint64_t ntc;
+    int32_t* mat_id;            /* per triangle: obj material id + 1 (main.cpp:185) */
+    float* kd;                  /* (nmat) x 3 diffuse colours, [0] = default (main.cpp:229-245) */
+    uint32_t nmat;
+} spt_mesh;
+
+/* ---------------------------------------------------------------- device */
+/* OptixBackend::init (optix_backend.h:178-186): select + initialise the GPU. */
+spt_status spt_init(int32_t device);
+
+/* OptixBackend::set_triangles_soup (optix_backend.h:283-364) + Scene::commit
+ * (main.cpp:312-318).  Host arrays; the library builds a binned-SAH BVH on
+ * the host and uploads it (the reference builds the GAS on device).
+ * pos_tri/nrm_tri/tc_tri: 3 x int32 per triangle; pos/nrm: 3 floats per
+ * entry; tc: 2 floats.  nrm_tri/tc_tri/mat_id may be NULL.  A normal index
+ * of -1 falls back to the geometric normal (the reference would gather out
+ * of bounds). */
+spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                            const int32_t* nrm_tri, const float* nrm, uint64_t nnrm,
+                            const int32_t* tc_tri, const float* tc, uint64_t ntc,
+                            const int32_t* mat_id, spt_scene* out);
+
+/* Per-material albedo (RGB, nmat x 3).  Default: 1 for every material, as in
+ * the reference (main.cpp:234,244 — Kd is read and discarded). */
+spt_status spt_scene_set_albedo(spt_scene scene, const float* albedo_rgb, uint32_t nmat);
+
+spt_status spt_scene_get_stats(spt_scene scene, spt_scene_stats* out);
+spt_status spt_scene_destroy(spt_scene scene);
+
+/* OptixBackend::intersect (optix_backend.h:422-460) → __raygen__rg
+ * (wavefront_isect.cu:80-112): one lane per ray; mask_size == 1 broadcasts
+ * mask[0]; masked lanes write nothing; a miss writes tri_id = -1 (t/u/v
+ * untouched); do_closest = 0 is OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT.
+ * All pointers are device pointers; n rays. */
+spt_status spt_intersect(spt_scene scene, const spt_rays* rays, const uint8_t* mask,
+                         uint32_t mask_size, const spt_hits* hits, uint32_t n,
+                         int32_t do_closest, void* stream);
+
+/* Hit reconstruction (optix_backend.h:462-486 + main.cpp:325): for lanes with
+ * tri_id != -1 && mask, fills the requested spt_hit_info planes. */
+spt_status spt_hit_info_compute(spt_scene scene, const spt_rays* rays, const spt_hits* hits,
+                                const uint8_t* mask, uint32_t mask_size, uint32_t n,
+                                const spt_hit_info* out, void* stream);
+
+/* main.cpp:354-429: the whole wavefront render of one tile.  film_dev is a
+ * device buffer of 3 x tile_rows x width floats (planar R, G, B as the
+ * reference's SpectrumC film, main.cpp:369), already divided by spp.  The
+ * call returns after the stream has drained.  stats may be NULL. */
+spt_status spt_render(spt_scene scene, const spt_render_params* params, float* film_dev,
+                      spt_render_stats* stats, void* stream);
+
+/* Rows of tile `tile_index` (in increasing order).  Returns the row count;
+ * writes at most `cap` row indices into rows (may be NULL). */
+uint32_t spt_tile_rows(uint32_t height, uint32_t tile_index, uint32_t tile_count,
+                       uint32_t rows_per_group, uint32_t* rows, uint32_t cap);
+
+/* Default parameters of the reference's main() (main.cpp:357-383). */
+void spt_default_params(spt_render_params* p);
+
+const char* spt_last_error(void);
+const char* spt_version(void);
+
+/* ------------------------------------------------------------------ host */
+/* load_meshes (main.cpp:141-251): triangulating OBJ reader with tinyobj's
+ * index semantics (position / normal / texcoord triplets, material id + 1). */
+spt_status spt_obj_load(const char* path, spt_mesh* out);
+void spt_mesh_free(spt_mesh* mesh);
+
+/* Fimage::save_pfm (fimage.h:33-58): planar R, G, B → interleaved,
+ * rows bottom-up, scale -1 (little endian). */
+spt_status spt_pfm_write(const char* path, const float* r, const float* g, const float* b,
+                         uint32_t width, uint32_t height);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPT_H */

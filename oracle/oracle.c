@@ -1,0 +1,619 @@
+/*
+ * oracle.c — CPU restatement of jamornsriwasansak/smallpt-enoki-optix's
+ * wavefront path tracer (the BASELINE.json north_star path).
+ *
+ * TEST INFRASTRUCTURE ONLY: the checker and the CPU baseline.  The product
+ * (smallpt-enoki-optix_amd/, libspt.so) never includes, links or calls it.
+ *
+ * Every function cites the reference file:line it restates (paths relative to
+ * the reference root).  Third-party arithmetic restated from published
+ * algorithms:
+ *   - PCG32 (Enoki include/enoki/random.h; canonical pcg32 by M. O'Neill) —
+ *     pinned by the canonical (42, 54) known-answer vector.
+ *   - sincos (Enoki array_math.h: Cephes single-precision sin/cos) — parity
+ *     unpinned (Enoki absent); our op order is fixed below and shared by
+ *     specification (not by code) with the HIP kernels.
+ *   - OptiX 7 closest-hit triangle test: restated as the Woop/Benthin/Wald
+ *     2013 watertight test with PBRT's double-precision edge fallback; the
+ *     barycentric convention is OptiX's p = (1-u-v) v0 + u v1 + v v2
+ *     (add_math.h:3-7).  Parity vs OptiX unpinned (OptiX absent).
+ * Floating-point: compiled with -ffp-contract=off; every fused multiply-add
+ * is an explicit fmaf().
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PCG32_MULT 0x5851f42d4c957f2dULL
+#define PI_F 3.14159265358979323846f
+
+/* ------------------------------------------------------------------ PCG32 */
+/* Enoki random.h (external): seed / next_uint32 / next_float32.  Seeding call
+ * site main.cpp:376 (initstate = PCG32_DEFAULT_STATE, initseq = pixel index). */
+typedef struct { uint64_t state, inc; } pcg32_t;
+
+static inline uint32_t pcg32_next(pcg32_t* r) {
+    uint64_t old = r->state;
+    r->state = old * PCG32_MULT + r->inc;
+    uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+static inline void pcg32_seed(pcg32_t* r, uint64_t initstate, uint64_t initseq) {
+    r->state = 0;
+    r->inc = (initseq << 1u) | 1u;
+    pcg32_next(r);
+    r->state += initstate;
+    pcg32_next(r);
+}
+static inline float u32_as_float(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+static inline uint32_t float_as_u32(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+static inline float pcg32_float(pcg32_t* r) {
+    return u32_as_float((pcg32_next(r) >> 9) | 0x3f800000u) - 1.0f;
+}
+
+void oracle_pcg32_seq(uint64_t initstate, uint64_t initseq, uint32_t* out, int32_t n) {
+    pcg32_t r; pcg32_seed(&r, initstate, initseq);
+    for (int32_t i = 0; i < n; i++) out[i] = pcg32_next(&r);
+}
+void oracle_pcg32_floats(uint64_t initstate, uint64_t initseq, float* out, int32_t n) {
+    pcg32_t r; pcg32_seed(&r, initstate, initseq);
+    for (int32_t i = 0; i < n; i++) out[i] = pcg32_float(&r);
+}
+
+/* ---------------------------------------------------------------- sincos */
+/* Cephes single-precision joint sin/cos as used by Enoki's sincos (called at
+ * mapping.h:9 and mapping.h:25). */
+void oracle_sincos(float x, float* s_out, float* c_out) {
+    float xa = fabsf(x);
+    int32_t j = (int32_t)(xa * 1.2732395447351626862f);
+    j = (j + 1) & ~1;
+    float y = (float)j;
+    uint32_t sign_sin = (((uint32_t)j << 29) & 0x80000000u) ^ (float_as_u32(x) & 0x80000000u);
+    uint32_t sign_cos = ((uint32_t)(~(j - 2)) << 29) & 0x80000000u;
+    y = ((xa - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    float z = y * y;
+    float s = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z;
+    float c = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f) * z;
+    s = fmaf(s, y, y);
+    c = fmaf(c, z, fmaf(z, -0.5f, 1.0f));
+    int poly = (j & 2) == 0;
+    float rs = poly ? s : c;
+    float rc = poly ? c : s;
+    *s_out = u32_as_float(float_as_u32(rs) ^ sign_sin);
+    *c_out = u32_as_float(float_as_u32(rc) ^ sign_cos);
+}
+
+/* ------------------------------------------------------------ vector math */
+typedef struct { float x, y, z; } v3;
+static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline float dot3(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+static inline v3 cross3(v3 a, v3 b) {
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+/* Enoki normalize: v * rsqrt(squared_norm(v)); restated as v * (1/sqrt). */
+static inline v3 normalize3(v3 v) {
+    float inv = 1.0f / sqrtf(dot3(v, v));
+    return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+static inline float get(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+/* Frame3 (coordframe.h:5-51): columns bx, by, bz; to_world = M * l. */
+typedef struct { v3 bx, by, bz; } frame3;
+static inline v3 to_world(const frame3* f, v3 l) {
+    return mk((f->bx.x * l.x + f->by.x * l.y) + f->bz.x * l.z,
+              (f->bx.y * l.x + f->by.y * l.y) + f->bz.y * l.z,
+              (f->bx.z * l.x + f->by.z * l.y) + f->bz.z * l.z);
+}
+static inline v3 to_local(const frame3* f, v3 w) {
+    return mk(dot3(f->bx, w), dot3(f->by, w), dot3(f->bz, w));
+}
+/* coordframe.h:17-30 — branchless ONB with the normal as local +y.  The
+ * normal is NOT renormalised (reference feeds an un-normalised interpolated
+ * shading normal, optix_backend.h:412-420). */
+static inline frame3 frame_from_normal(v3 n) {
+    float sign = copysignf(1.0f, n.y);
+    float a = -1.0f / (sign + n.y);
+    float b = (n.z * n.x) * a;
+    frame3 f;
+    f.bx = mk(sign + (n.x * n.x) * a, -n.x, b);
+    f.by = n;
+    f.bz = mk(sign * b, (-sign) * n.z, 1.0f + ((sign * n.z) * n.z) * a);
+    return f;
+}
+void oracle_frame_to_world(const float* n3, const float* l3, float* out3) {
+    frame3 f = frame_from_normal(mk(n3[0], n3[1], n3[2]));
+    v3 w = to_world(&f, mk(l3[0], l3[1], l3[2]));
+    out3[0] = w.x; out3[1] = w.y; out3[2] = w.z;
+}
+
+/* mapping.h:5-11 */
+static inline v3 cosine_hemisphere(float xi_x, float xi_y) {
+    float sin_phi = sqrtf(1.0f - xi_x);
+    float theta = (PI_F * 2.0f) * xi_y;
+    float s, c;
+    oracle_sincos(theta, &s, &c);
+    return mk(c * sin_phi, sqrtf(xi_x), s * sin_phi);
+}
+void oracle_cosine_hemisphere(float xi_x, float xi_y, float* out3) {
+    v3 r = cosine_hemisphere(xi_x, xi_y);
+    out3[0] = r.x; out3[1] = r.y; out3[2] = r.z;
+}
+/* mapping.h:15-27 (Shirley-Chiu concentric map via Dave Cline). */
+static inline void disk_from_square(float xi_x, float xi_y, float* ox, float* oy) {
+    float ax = xi_x * 2.0f - 1.0f, ay = xi_y * 2.0f - 1.0f;
+    float ax2 = ax * ax, ay2 = ay * ay;
+    int cond = ax2 > ay2;
+    float r = cond ? ax : ay;
+    float phi = cond ? (PI_F / 4.0f) * (ay / ax) : (PI_F / 2.0f) - (PI_F / 4.0f) * (ax / ay);
+    float s, c;
+    oracle_sincos(phi, &s, &c);
+    *ox = r * c;
+    *oy = r * s;
+}
+void oracle_disk_from_square(float xi_x, float xi_y, float* out2) {
+    disk_from_square(xi_x, xi_y, &out2[0], &out2[1]);
+}
+
+/* ----------------------------------------------------------------- camera */
+/* ThinlensCamera (pinhole.h:7-72). */
+typedef struct {
+    v3 origin;
+    frame3 frame;
+    float lens_radius, focal_dist, dist_lens_to_film, ratio, film_y;
+    int32_t W, H;
+} camera_t;
+
+static void camera_setup(camera_t* c, const oracle_params* p) {
+    v3 from = mk(p->look_from[0], p->look_from[1], p->look_from[2]);
+    v3 at = mk(p->look_at[0], p->look_at[1], p->look_at[2]);
+    v3 up = mk(p->up[0], p->up[1], p->up[2]);
+    c->origin = from;
+    v3 z = normalize3(sub(at, from));          /* pinhole.h:20 */
+    v3 x = normalize3(cross3(up, z));          /* pinhole.h:21 */
+    v3 y = normalize3(cross3(z, x));           /* pinhole.h:22 */
+    c->frame.bx = x; c->frame.by = y; c->frame.bz = z;
+    c->lens_radius = p->lens_radius;
+    c->focal_dist = p->focal_dist;
+    c->film_y = p->film_size_y;
+    c->dist_lens_to_film = (p->film_size_y * 0.5f) / tanf(p->fov_y * 0.5f); /* pinhole.h:40 */
+    c->ratio = (float)p->width / (float)p->height;                         /* pinhole.h:41 */
+    c->W = p->width; c->H = p->height;
+}
+/* pinhole.h:27-32 */
+static v3 camera_sample_pos(const camera_t* c, float xi_x, float xi_y) {
+    float lx, ly;
+    disk_from_square(xi_x, xi_y, &lx, &ly);
+    lx = lx * c->lens_radius; ly = ly * c->lens_radius;
+    v3 w = to_world(&c->frame, mk(lx, 0.0f, ly));
+    return mk(w.x + c->origin.x, w.y + c->origin.y, w.z + c->origin.z);
+}
+/* pinhole.h:34-56 */
+static v3 camera_sample_dir(const camera_t* c, int32_t px, int32_t py, v3 pos, float xi_x, float xi_y) {
+    v3 lens = to_local(&c->frame, sub(pos, c->origin));
+    float ndc_x = ((float)px + xi_x) / (float)c->W;
+    float ndc_y = ((float)py + xi_y) / (float)c->H;
+    float fx = (0.5f - ndc_x) * (c->ratio * c->film_y);
+    float fy = (0.5f - ndc_y) * c->film_y;
+    float fz = c->dist_lens_to_film;
+    v3 focal = mk((c->focal_dist * fx) / fz, (c->focal_dist * fy) / fz, (c->focal_dist * fz) / fz);
+    v3 d = normalize3(sub(focal, lens));
+    return to_world(&c->frame, d);
+}
+void oracle_camera_ray(const oracle_params* p, int32_t px, int32_t py, const float* xi4,
+                       float* org3, float* dir3, float* basis9) {
+    camera_t c;
+    camera_setup(&c, p);
+    v3 o = camera_sample_pos(&c, xi4[0], xi4[1]);
+    v3 d = camera_sample_dir(&c, px, py, o, xi4[2], xi4[3]);
+    org3[0] = o.x; org3[1] = o.y; org3[2] = o.z;
+    dir3[0] = d.x; dir3[1] = d.y; dir3[2] = d.z;
+    if (basis9) {
+        basis9[0] = c.frame.bx.x; basis9[1] = c.frame.bx.y; basis9[2] = c.frame.bx.z;
+        basis9[3] = c.frame.by.x; basis9[4] = c.frame.by.y; basis9[5] = c.frame.by.z;
+        basis9[6] = c.frame.bz.x; basis9[7] = c.frame.bz.y; basis9[8] = c.frame.bz.z;
+    }
+}
+
+/* ------------------------------------------------------------------ scene */
+typedef struct {
+    float bmin[3], bmax[3];
+    int32_t left;   /* inner: index of left child (right = left + 1); leaf: first prim */
+    int32_t count;  /* 0 = inner */
+} onode;
+
+typedef struct {
+    int64_t ntri;
+    float* v;       /* ntri * 9: v0 v1 v2 */
+    float* n;       /* ntri * 9: shading normals n0 n1 n2 */
+    int32_t* mat;   /* ntri */
+    float* albedo;  /* nmat * 3 */
+    int32_t nmat;
+    int32_t use_bvh;
+    onode* nodes;
+    int64_t nnodes;
+    int32_t* prims; /* leaf order -> triangle id */
+} oscene;
+
+typedef struct { float* cen; int32_t axis; } sortctx;
+static __thread sortctx g_sort;
+static int cmp_prim(const void* a, const void* b) {
+    float ca = g_sort.cen[*(const int32_t*)a * 3 + g_sort.axis];
+    float cb = g_sort.cen[*(const int32_t*)b * 3 + g_sort.axis];
+    if (ca < cb) return -1;
+    if (ca > cb) return 1;
+    return (*(const int32_t*)a < *(const int32_t*)b) ? -1 : 1;
+}
+
+/* Median-split BVH (independent of the product's binned-SAH BVH). */
+static void build_node(oscene* s, float* cen, int64_t ni, int64_t first, int64_t count) {
+    onode* nd = &s->nodes[ni];
+    for (int k = 0; k < 3; k++) { nd->bmin[k] = INFINITY; nd->bmax[k] = -INFINITY; }
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = first; i < first + count; i++) {
+        int32_t p = s->prims[i];
+        for (int vtx = 0; vtx < 3; vtx++)
+            for (int k = 0; k < 3; k++) {
+                float x = s->v[p * 9 + vtx * 3 + k];
+                if (x < nd->bmin[k]) nd->bmin[k] = x;
+                if (x > nd->bmax[k]) nd->bmax[k] = x;
+            }
+        for (int k = 0; k < 3; k++) {
+            float c = cen[p * 3 + k];
+            if (c < cmin[k]) cmin[k] = c;
+            if (c > cmax[k]) cmax[k] = c;
+        }
+    }
+    if (count <= 4) { nd->left = (int32_t)first; nd->count = (int32_t)count; return; }
+    int axis = 0;
+    float ext[3] = {cmax[0] - cmin[0], cmax[1] - cmin[1], cmax[2] - cmin[2]};
+    if (ext[1] > ext[axis]) axis = 1;
+    if (ext[2] > ext[axis]) axis = 2;
+    g_sort.cen = cen; g_sort.axis = axis;
+    qsort(&s->prims[first], (size_t)count, sizeof(int32_t), cmp_prim);
+    int64_t half = count / 2;
+    int64_t l = s->nnodes;
+    s->nnodes += 2;
+    nd->left = (int32_t)l;
+    nd->count = 0;
+    build_node(s, cen, l, first, half);
+    build_node(s, cen, l + 1, first + half, count - half);
+}
+
+void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nvert, int64_t ntri,
+                          const int32_t* nrm_tri, const float* nrm, int64_t nnrm,
+                          const int32_t* mat_id, const float* albedo, int32_t nmat,
+                          int32_t use_bvh) {
+    oscene* s = (oscene*)calloc(1, sizeof(oscene));
+    s->ntri = ntri;
+    s->use_bvh = use_bvh;
+    s->v = (float*)malloc(sizeof(float) * 9 * (size_t)(ntri > 0 ? ntri : 1));
+    s->n = (float*)malloc(sizeof(float) * 9 * (size_t)(ntri > 0 ? ntri : 1));
+    s->mat = (int32_t*)malloc(sizeof(int32_t) * (size_t)(ntri > 0 ? ntri : 1));
+    for (int64_t t = 0; t < ntri; t++) {
+        for (int vtx = 0; vtx < 3; vtx++) {
+            int32_t pi = pos_tri[t * 3 + vtx];
+            for (int k = 0; k < 3; k++)
+                s->v[t * 9 + vtx * 3 + k] = (pi >= 0 && pi < nvert) ? pos[pi * 3 + k] : NAN;
+        }
+        /* A vertex without a normal (index -1) takes the geometric normal
+         * normalize(cross(v1 - v0, v2 - v0)) (add_math.h:9-16); the reference
+         * would gather out of bounds there. */
+        const float* tv = &s->v[t * 9];
+        v3 g = normalize3(cross3(mk(tv[3] - tv[0], tv[4] - tv[1], tv[5] - tv[2]),
+                                 mk(tv[6] - tv[0], tv[7] - tv[1], tv[8] - tv[2])));
+        for (int vtx = 0; vtx < 3; vtx++) {
+            int32_t qi = nrm_tri ? nrm_tri[t * 3 + vtx] : -1;
+            int ok = qi >= 0 && qi < nnrm;
+            s->n[t * 9 + vtx * 3 + 0] = ok ? nrm[qi * 3 + 0] : g.x;
+            s->n[t * 9 + vtx * 3 + 1] = ok ? nrm[qi * 3 + 1] : g.y;
+            s->n[t * 9 + vtx * 3 + 2] = ok ? nrm[qi * 3 + 2] : g.z;
+        }
+        s->mat[t] = mat_id ? mat_id[t] : 0;
+    }
+    s->nmat = nmat > 0 ? nmat : 1;
+    s->albedo = (float*)malloc(sizeof(float) * 3 * (size_t)s->nmat);
+    for (int32_t m = 0; m < s->nmat; m++)
+        for (int k = 0; k < 3; k++) s->albedo[m * 3 + k] = (albedo && nmat > 0) ? albedo[m * 3 + k] : 1.0f;
+    if (use_bvh && ntri > 0) {
+        float* cen = (float*)malloc(sizeof(float) * 3 * (size_t)ntri);
+        for (int64_t t = 0; t < ntri; t++)
+            for (int k = 0; k < 3; k++)
+                cen[t * 3 + k] = (s->v[t * 9 + k] + s->v[t * 9 + 3 + k] + s->v[t * 9 + 6 + k]) * (1.0f / 3.0f);
+        s->prims = (int32_t*)malloc(sizeof(int32_t) * (size_t)ntri);
+        for (int64_t t = 0; t < ntri; t++) s->prims[t] = (int32_t)t;
+        s->nodes = (onode*)malloc(sizeof(onode) * (size_t)(2 * ntri + 1));
+        s->nnodes = 1;
+        build_node(s, cen, 0, 0, ntri);
+        free(cen);
+    }
+    return s;
+}
+
+void oracle_scene_destroy(void* scene) {
+    oscene* s = (oscene*)scene;
+    if (!s) return;
+    free(s->v); free(s->n); free(s->mat); free(s->albedo); free(s->nodes); free(s->prims);
+    free(s);
+}
+
+/* ------------------------------------------------------ triangle (Woop) */
+typedef struct {
+    float o[3], d[3];
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+    float inv[3];
+} wray;
+
+static inline void wray_setup(wray* r) {
+    float ax = fabsf(r->d[0]), ay = fabsf(r->d[1]), az = fabsf(r->d[2]);
+    int kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    if (r->d[kz] < 0.0f) { int tmp = kx; kx = ky; ky = tmp; }
+    r->kx = kx; r->ky = ky; r->kz = kz;
+    r->Sx = r->d[kx] / r->d[kz];
+    r->Sy = r->d[ky] / r->d[kz];
+    r->Sz = 1.0f / r->d[kz];
+    for (int k = 0; k < 3; k++) r->inv[k] = 1.0f / r->d[k];
+}
+
+/* Returns 1 and t/u/v when the triangle is hit with t in [tmin, tmax]. */
+static inline int woop_test(const wray* r, const float* tv, float tmin, float tmax,
+                            float* t_out, float* u_out, float* v_out) {
+    float A[3], B[3], C[3];
+    for (int k = 0; k < 3; k++) {
+        A[k] = tv[k] - r->o[k];
+        B[k] = tv[3 + k] - r->o[k];
+        C[k] = tv[6 + k] - r->o[k];
+    }
+    float Ax = A[r->kx] - r->Sx * A[r->kz], Ay = A[r->ky] - r->Sy * A[r->kz];
+    float Bx = B[r->kx] - r->Sx * B[r->kz], By = B[r->ky] - r->Sy * B[r->kz];
+    float Cx = C[r->kx] - r->Sx * C[r->kz], Cy = C[r->ky] - r->Sy * C[r->kz];
+    float U = Cx * By - Cy * Bx;
+    float V = Ax * Cy - Ay * Cx;
+    float W = Bx * Ay - By * Ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        U = (float)((double)Cx * (double)By - (double)Cy * (double)Bx);
+        V = (float)((double)Ax * (double)Cy - (double)Ay * (double)Cx);
+        W = (float)((double)Bx * (double)Ay - (double)By * (double)Ax);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return 0;
+    float det = (U + V) + W;
+    if (det == 0.0f) return 0;
+    float Az = r->Sz * A[r->kz], Bz = r->Sz * B[r->kz], Cz = r->Sz * C[r->kz];
+    float T = (U * Az + V * Bz) + W * Cz;
+    float t = T / det;
+    if (!(t >= tmin && t <= tmax)) return 0;
+    *t_out = t;
+    *u_out = V / det;
+    *v_out = W / det;
+    return 1;
+}
+
+#define BOX_PAD 1.000001f
+static inline int box_test(const wray* r, const onode* nd, float tmin, float tmax) {
+    float tn = tmin, tf = tmax;
+    for (int k = 0; k < 3; k++) {
+        float t0 = (nd->bmin[k] - r->o[k]) * r->inv[k];
+        float t1 = (nd->bmax[k] - r->o[k]) * r->inv[k];
+        float lo = fminf(t0, t1), hi = fmaxf(t0, t1) * BOX_PAD;
+        tn = fmaxf(tn, lo);
+        tf = fminf(tf, hi);
+    }
+    return tn <= tf;
+}
+
+typedef struct { int32_t id; float t, u, v; } ohit;
+
+/* Closest hit over [tmin, tmax]; equal t broken toward the smaller triangle id
+ * so the result is independent of traversal order (OptiX returns one of the
+ * tied hits; we fix the choice). */
+static inline void consider(const oscene* s, const wray* r, int32_t p, float tmin, ohit* h) {
+    float t, u, v;
+    if (woop_test(r, &s->v[(int64_t)p * 9], tmin, h->t, &t, &u, &v)) {
+        if (t < h->t || h->id < 0 || p < h->id) { h->id = p; h->t = t; h->u = u; h->v = v; }
+    }
+}
+
+static void trace(const oscene* s, const wray* r, float tmin, float tmax, int closest, ohit* h) {
+    h->id = -1; h->t = tmax; h->u = 0; h->v = 0;
+    if (s->ntri <= 0) return;
+    if (!s->use_bvh) {
+        for (int64_t p = 0; p < s->ntri; p++) {
+            consider(s, r, (int32_t)p, tmin, h);
+            if (!closest && h->id >= 0) return;
+        }
+        return;
+    }
+    int32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const onode* nd = &s->nodes[stack[--sp]];
+        if (!box_test(r, nd, tmin, h->t)) continue;
+        if (nd->count) {
+            for (int32_t i = 0; i < nd->count; i++) {
+                consider(s, r, s->prims[nd->left + i], tmin, h);
+                if (!closest && h->id >= 0) return;
+            }
+        } else {
+            stack[sp++] = nd->left + 1;
+            stack[sp++] = nd->left;
+        }
+    }
+}
+
+/* ------------------------------------------------------ thread helpers */
+typedef struct {
+    void (*fn)(void* ctx, int64_t i);
+    void* ctx;
+    int64_t n;
+    atomic_llong next;
+    int64_t chunk;
+} pfor_t;
+static void* pfor_worker(void* arg) {
+    pfor_t* p = (pfor_t*)arg;
+    for (;;) {
+        int64_t b = atomic_fetch_add(&p->next, p->chunk);
+        if (b >= p->n) break;
+        int64_t e = b + p->chunk < p->n ? b + p->chunk : p->n;
+        for (int64_t i = b; i < e; i++) p->fn(p->ctx, i);
+    }
+    return NULL;
+}
+static void parallel_for(int64_t n, int64_t chunk, int nthreads, void (*fn)(void*, int64_t), void* ctx) {
+    pfor_t p;
+    p.fn = fn; p.ctx = ctx; p.n = n; p.chunk = chunk < 1 ? 1 : chunk;
+    atomic_init(&p.next, 0);
+    if (nthreads <= 1) { pfor_worker(&p); return; }
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, pfor_worker, &p);
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(th);
+}
+
+/* ------------------------------------------------------------ intersect */
+typedef struct {
+    const oscene* s;
+    const float *ox, *oy, *oz, *dx, *dy, *dz, *tmin, *tmax;
+    const uint8_t* mask; uint32_t mask_size;
+    int32_t* id; float *t, *u, *v;
+    int closest;
+} isect_ctx;
+static void isect_one(void* c_, int64_t i) {
+    isect_ctx* c = (isect_ctx*)c_;
+    uint8_t m = (c->mask_size == 1) ? c->mask[0] : c->mask[i];  /* wavefront_isect.cu:86 */
+    if (!m) return;                                              /* masked lanes untouched */
+    wray r;
+    r.o[0] = c->ox[i]; r.o[1] = c->oy[i]; r.o[2] = c->oz[i];
+    r.d[0] = c->dx[i]; r.d[1] = c->dy[i]; r.d[2] = c->dz[i];
+    wray_setup(&r);
+    ohit h;
+    trace(c->s, &r, c->tmin[i], c->tmax[i], c->closest, &h);
+    c->id[i] = h.id;                                             /* -1 on miss (wavefront_isect.cu:70) */
+    if (h.id >= 0) { c->t[i] = h.t; c->u[i] = h.u; c->v[i] = h.v; }
+}
+void oracle_intersect(void* scene, const float* ox, const float* oy, const float* oz,
+                      const float* dx, const float* dy, const float* dz,
+                      const float* tmin, const float* tmax, const uint8_t* mask,
+                      uint32_t mask_size, int32_t* tri_id, float* t, float* u, float* v,
+                      int64_t n, int32_t do_closest, int32_t nthreads) {
+    isect_ctx c = {(const oscene*)scene, ox, oy, oz, dx, dy, dz, tmin, tmax, mask, mask_size,
+                   tri_id, t, u, v, do_closest};
+    parallel_for(n, 256, nthreads, isect_one, &c);
+}
+
+/* --------------------------------------------------------------- render */
+/* Russian-roulette side stream (build addition, absent in the reference —
+ * SURVEY F7/A14): a counter-based hash so the 4+2D PCG32 layout is untouched. */
+static inline float rr_uniform(uint32_t pixel, uint32_t sample, uint32_t depth) {
+    uint32_t h = pixel * 0x9E3779B1u ^ (sample + 0x7F4A7C15u) * 0x85EBCA77u ^ (depth + 1u) * 0xC2B2AE3Du;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+typedef struct {
+    const oscene* s;
+    const oracle_params* p;
+    camera_t cam;
+    const int32_t* rows;
+    float* film;
+    int64_t nrow_pixels;
+    atomic_llong casts;
+} render_ctx;
+
+static inline void draw2(pcg32_t* rng, int order, float* x, float* y) {
+    float a = pcg32_float(rng);
+    float b = pcg32_float(rng);
+    if (order == 0) { *y = a; *x = b; } else { *x = a; *y = b; }
+}
+
+static void render_pixel(void* c_, int64_t li) {
+    render_ctx* c = (render_ctx*)c_;
+    const oracle_params* p = c->p;
+    const oscene* s = c->s;
+    int32_t W = p->width;
+    int64_t lrow = li / W;
+    int32_t px = (int32_t)(li % W);
+    int32_t py = c->rows[lrow];
+    uint32_t pixel = (uint32_t)py * (uint32_t)W + (uint32_t)px;   /* main.cpp:379-382 */
+    pcg32_t rng;
+    pcg32_seed(&rng, p->rng_initstate, (uint64_t)pixel);          /* main.cpp:376 */
+    float film[3] = {0.0f, 0.0f, 0.0f};
+    long long casts = 0;
+    for (int32_t smp = 0; smp < p->spp; smp++) {                  /* main.cpp:385 */
+        float contrib[3] = {1.0f, 1.0f, 1.0f};                    /* main.cpp:391 */
+        int active = 1;                                           /* main.cpp:392 */
+        float xi_x, xi_y;
+        draw2(&rng, p->rng_order, &xi_x, &xi_y);                  /* main.cpp:395 */
+        v3 o = camera_sample_pos(&c->cam, xi_x, xi_y);
+        draw2(&rng, p->rng_order, &xi_x, &xi_y);                  /* main.cpp:396 */
+        v3 d = camera_sample_dir(&c->cam, px, py, o, xi_x, xi_y);
+        for (int32_t j = 0; j < p->max_depth; j++) {              /* main.cpp:399 */
+            ohit h; h.id = -1;
+            if (active) {                                          /* main.cpp:402-404 */
+                wray r;
+                r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z;
+                r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z;
+                wray_setup(&r);
+                trace(s, &r, 0.001f, 1e20f, 1, &h);               /* ray.h:15-17 */
+                casts++;
+                if (h.id < 0) {                                   /* main.cpp:407 */
+                    for (int k = 0; k < 3; k++) film[k] = film[k] + contrib[k] * p->env[k];
+                }
+            }
+            active = active && (h.id >= 0);                       /* main.cpp:410 */
+            draw2(&rng, p->rng_order, &xi_x, &xi_y);              /* main.cpp:413 (always drawn) */
+            if (!active) continue;
+            /* optix_backend.h:469 (position), :483-484 (interpolated shading normal) */
+            const float* nv = &s->n[(int64_t)h.id * 9];
+            float w = (1.0f - h.u) - h.v;
+            v3 n = mk((w * nv[0] + h.u * nv[3]) + h.v * nv[6],
+                      (w * nv[1] + h.u * nv[4]) + h.v * nv[7],
+                      (w * nv[2] + h.u * nv[5]) + h.v * nv[8]);
+            v3 hp = mk(o.x + h.t * d.x, o.y + h.t * d.y, o.z + h.t * d.z);
+            frame3 f = frame_from_normal(n);                      /* main.cpp:414 */
+            v3 lo = cosine_hemisphere(xi_x, xi_y);                /* main.cpp:418, :109-117 */
+            v3 out = to_world(&f, lo);                            /* main.cpp:419 */
+            int32_t m = s->mat[h.id];
+            if (m < 0 || m >= s->nmat) m = 0;
+            for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * s->albedo[m * 3 + k]; /* :422 */
+            o = hp;                                               /* main.cpp:423 */
+            d = out;                                              /* main.cpp:424 */
+            if (j + 1 >= p->rr_start_depth && j + 1 < p->max_depth) {
+                float q = fmaxf(contrib[0], fmaxf(contrib[1], contrib[2]));
+                if (q < 1.0f) {
+                    if (rr_uniform(pixel, (uint32_t)smp, (uint32_t)j) >= q) { active = 0; continue; }
+                    for (int k = 0; k < 3; k++) contrib[k] = contrib[k] / q;
+                }
+            }
+        }
+    }
+    int64_t npx = c->nrow_pixels;
+    for (int k = 0; k < 3; k++) c->film[k * npx + li] = film[k] / (float)p->spp; /* main.cpp:429 */
+    atomic_fetch_add(&c->casts, casts);
+}
+
+int oracle_render(void* scene, const oracle_params* p, const int32_t* rows, int32_t nrows,
+                  float* film, int32_t nthreads, uint64_t* ray_casts_out) {
+    if (!scene || !p || p->width <= 0 || p->height <= 0 || p->spp <= 0 || p->max_depth <= 0) return -1;
+    for (int32_t i = 0; i < nrows; i++)
+        if (rows[i] < 0 || rows[i] >= p->height) return -2;
+    render_ctx c;
+    c.s = (const oscene*)scene;
+    c.p = p;
+    camera_setup(&c.cam, p);
+    c.rows = rows;
+    c.film = film;
+    c.nrow_pixels = (int64_t)nrows * p->width;
+    atomic_init(&c.casts, 0);
+    parallel_for(c.nrow_pixels, 64, nthreads, render_pixel, &c);
+    if (ray_casts_out) *ray_casts_out = (uint64_t)atomic_load(&c.casts);
+    return 0;
+}

@@ -1,0 +1,65 @@
+/*
+ * oracle.h — CPU restatement of the reference path tracer.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (libspt.so, the HIP kernels,
+ * the host driver) links, includes or calls this code.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it, as the
+ * checker / CPU baseline.
+ *
+ * Parity status: PCG32 is pinned by the canonical pcg32 known-answer vector
+ * (tests/test_oracle.py).  The reference itself cannot be built in this
+ * container (no CUDA, OptiX, Enoki or tinyobjloader; DiffuseBsdf undefined at
+ * main.cpp:234) and ships no tests or golden vectors, so the geometry /
+ * shading arithmetic is "parity unpinned" beyond the analytic and
+ * formula-derived known answers in tests/test_oracle.py.
+ */
+#ifndef SPT_ORACLE_H
+#define SPT_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_params {
+    int32_t width, height, spp, max_depth;   /* main.cpp:357-361 (max_depth = ray casts) */
+    float look_from[3], look_at[3], up[3];   /* main.cpp:383 */
+    float lens_radius, focal_dist, fov_y, film_size_y; /* pinhole.h:9-16 */
+    int32_t rng_order;       /* 0 = y-first (MSVC/GCC arg order), 1 = x-first */
+    int32_t rr_start_depth;  /* RR from this cast index on; >= max_depth disables */
+    float env[3];            /* sky radiance on miss (main.cpp:407 = 1) */
+    uint64_t rng_initstate;  /* PCG32_DEFAULT_STATE (main.cpp:376) */
+} oracle_params;
+
+void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nvert, int64_t ntri,
+                          const int32_t* nrm_tri, const float* nrm, int64_t nnrm,
+                          const int32_t* mat_id, const float* albedo, int32_t nmat,
+                          int32_t use_bvh);
+void oracle_scene_destroy(void* scene);
+
+/* wavefront_isect.cu:80-112 semantics: masked lanes untouched; miss -> id -1. */
+void oracle_intersect(void* scene, const float* ox, const float* oy, const float* oz,
+                      const float* dx, const float* dy, const float* dz,
+                      const float* tmin, const float* tmax, const uint8_t* mask,
+                      uint32_t mask_size, int32_t* tri_id, float* t, float* u, float* v,
+                      int64_t n, int32_t do_closest, int32_t nthreads);
+
+/* main.cpp:354-446.  Renders rows[0..nrows) (global row indices) into
+ * film[3][nrows][width] (planar RGB, already divided by spp). */
+int oracle_render(void* scene, const oracle_params* p, const int32_t* rows, int32_t nrows,
+                  float* film, int32_t nthreads, uint64_t* ray_casts_out);
+
+/* Known-answer helpers. */
+void oracle_pcg32_seq(uint64_t initstate, uint64_t initseq, uint32_t* out, int32_t n);
+void oracle_pcg32_floats(uint64_t initstate, uint64_t initseq, float* out, int32_t n);
+void oracle_camera_ray(const oracle_params* p, int32_t px, int32_t py, const float* xi4,
+                       float* org3, float* dir3, float* basis9);
+void oracle_sincos(float x, float* s, float* c);
+void oracle_cosine_hemisphere(float xi_x, float xi_y, float* out3);
+void oracle_disk_from_square(float xi_x, float xi_y, float* out2);
+void oracle_frame_to_world(const float* n3, const float* local3, float* out3);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

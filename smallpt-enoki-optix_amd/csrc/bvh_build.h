@@ -1,0 +1,32 @@
+// bvh_build.h — host binned-SAH BVH2 builder.
+//
+// Replaces the OptiX GAS build (optixAccelBuild + optixAccelCompact,
+// optix_backend.h:283-364).  Output layout (64 B per node, 4 x float4) keeps
+// both children's boxes in the parent so one node fetch tests two boxes:
+//   [0] c0.lo.x c0.hi.x c0.lo.y c0.hi.y
+//   [1] c1.lo.x c1.hi.x c1.lo.y c1.hi.y
+//   [2] c0.lo.z c0.hi.z c1.lo.z c1.hi.z
+//   [3] c0 code, c1 code (int32 bits), 0, 0
+// child code >= 0: inner node index; < 0: leaf ~(first_slot << 3 | (count-1)).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace spt {
+
+constexpr uint32_t kMaxLeafSize = 8;    // 3 count bits in the leaf code
+constexpr uint32_t kMaxTriangles = 1u << 28;
+
+struct BvhBuildResult {
+    std::vector<float> nodes;        // 16 floats per node
+    std::vector<uint32_t> slot2tri;  // leaf order slot -> original triangle id
+    uint32_t max_depth = 0;          // deepest leaf (root = 0)
+    uint64_t leaves = 0;
+    uint32_t max_leaf = 0;
+    double sah_cost = 0.0;
+};
+
+// tri_verts: ntri x 9 floats (v0 v1 v2).  ntri == 0 gives an empty result.
+BvhBuildResult build_bvh(const float* tri_verts, uint64_t ntri);
+
+}  // namespace spt

@@ -1,0 +1,586 @@
+// capi.cpp — the C ABI (include/spt.h): scene upload, public intersect,
+// hit reconstruction and the wavefront render loop (main.cpp:354-429).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/spt.h"
+#include "bvh_build.h"
+#include "spt_internal.h"
+
+using namespace spt;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+spt_status fail(spt_status code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(call)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (call);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(e_ == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP, "HIP call '%s' failed: %s (%s:%d)", \
+                        #call, hipGetErrorString(e_), __FILE__, __LINE__);                         \
+    } while (0)
+
+template <typename T>
+void hfree(T*& p) {
+    if (p) (void)hipFree((void*)p);
+    p = nullptr;
+}
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// 52 B per path: rng u64 | 6 ray f32 | pix u32 | meta u32 | 3 throughput f32
+constexpr size_t kPathBytes = 8 + 6 * 4 + 4 + 4 + 3 * 4;
+constexpr size_t kHitBytes = 16;
+
+PathQueue carve_queue(char* base, size_t cap) {
+    PathQueue q;
+    q.rng = (uint64_t*)base;
+    float* f = (float*)(base + 8 * cap);
+    q.ox = f; q.oy = f + cap; q.oz = f + 2 * cap;
+    q.dx = f + 3 * cap; q.dy = f + 4 * cap; q.dz = f + 5 * cap;
+    q.pix = (uint32_t*)(f + 6 * cap);
+    q.meta = q.pix + cap;
+    q.tr = (float*)(q.meta + cap); q.tg = q.tr + cap; q.tb = q.tg + cap;
+    return q;
+}
+
+struct Workspace {
+    size_t cap = 0, film_cap = 0;
+    char* qa = nullptr;
+    char* qb = nullptr;
+    char* hits = nullptr;
+    float* film = nullptr;
+    uint32_t* counts = nullptr;             // [0], [1] queue counts
+    unsigned long long* stats = nullptr;    // casts, continuations, regenerations
+    uint32_t* host_counts = nullptr;        // pinned, 2 slots
+    std::vector<hipEvent_t> events;
+    hipEvent_t count_ev[2] = {nullptr, nullptr};
+
+    void release() {
+        hfree(qa); hfree(qb); hfree(hits); hfree(film); hfree(counts);
+        if (host_counts) (void)hipHostFree(host_counts);
+        for (auto e : events) (void)hipEventDestroy(e);
+        for (auto& e : count_ev) if (e) (void)hipEventDestroy(e);
+        *this = Workspace();
+    }
+};
+
+}  // namespace
+
+struct spt_scene_t {
+    int device = 0;
+    uint64_t ntri = 0;
+    float4* nodes = nullptr;
+    float4* tris = nullptr;
+    float4* snrm = nullptr;
+    float* tc = nullptr;
+    int32_t* orig2slot = nullptr;
+    float* albedo = nullptr;
+    uint32_t nmat = 1;
+    uint32_t stack_depth = 1;
+    spt_scene_stats stats{};
+    Workspace ws;
+
+    DeviceScene dev() const {
+        DeviceScene d;
+        d.nodes = nodes; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
+        d.albedo = albedo; d.nmat = nmat; d.stack_depth = stack_depth; d.empty = ntri == 0;
+        return d;
+    }
+    void release() {
+        ws.release();
+        hfree(nodes); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
+    }
+};
+
+namespace {
+
+spt_status ensure_device() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(SPT_ERR_NO_DEVICE, "no HIP device visible (%s)", hipGetErrorString(e));
+    return SPT_OK;
+}
+
+template <typename T>
+spt_status upload(T** dst, const void* src, size_t bytes) {
+    *dst = nullptr;
+    if (bytes == 0) return SPT_OK;
+    HIP_TRY(hipMalloc((void**)dst, bytes));
+    HIP_TRY(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    return SPT_OK;
+}
+
+// ThinlensCamera constructor (pinhole.h:9-25) + the per-call constants of
+// sample_dir (pinhole.h:40-41), evaluated once on the host.
+Camera make_camera(const spt_render_params& p) {
+    const spt_camera& c = p.camera;
+    Camera cam;
+    V3 from = v3(c.look_from[0], c.look_from[1], c.look_from[2]);
+    V3 at = v3(c.look_at[0], c.look_at[1], c.look_at[2]);
+    V3 up = v3(c.up[0], c.up[1], c.up[2]);
+    cam.origin = from;
+    V3 z = normalize(at - from);
+    V3 x = normalize(cross(up, z));
+    V3 y = normalize(cross(z, x));
+    cam.frame.bx = x; cam.frame.by = y; cam.frame.bz = z;
+    cam.lens_radius = c.lens_radius;
+    cam.focal_dist = c.focal_dist;
+    cam.film_y = c.film_size_y;
+    cam.dist_lens_to_film = (c.film_size_y * 0.5f) / std::tan(c.fov_y * 0.5f);
+    cam.ratio = (float)p.width / (float)p.height;
+    cam.fw = (float)p.width;
+    cam.fh = (float)p.height;
+    return cam;
+}
+
+spt_status ensure_workspace(Workspace& ws, size_t cap, size_t film_floats) {
+    if (cap > ws.cap) {
+        hfree(ws.qa); hfree(ws.qb); hfree(ws.hits);
+        ws.cap = 0;
+        HIP_TRY(hipMalloc((void**)&ws.qa, kPathBytes * cap));
+        HIP_TRY(hipMalloc((void**)&ws.qb, kPathBytes * cap));
+        HIP_TRY(hipMalloc((void**)&ws.hits, kHitBytes * cap));
+        ws.cap = cap;
+    }
+    if (film_floats > ws.film_cap) {
+        hfree(ws.film);
+        ws.film_cap = 0;
+        HIP_TRY(hipMalloc((void**)&ws.film, sizeof(float) * film_floats));
+        ws.film_cap = film_floats;
+    }
+    if (!ws.counts) {
+        HIP_TRY(hipMalloc((void**)&ws.counts, 64));
+        ws.stats = (unsigned long long*)((char*)ws.counts + 16);
+    }
+    if (!ws.host_counts) HIP_TRY(hipHostMalloc((void**)&ws.host_counts, 16, hipHostMallocDefault));
+    for (auto& e : ws.count_ev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return SPT_OK;
+}
+
+spt_status get_event(Workspace& ws, size_t idx, hipEvent_t* out) {
+    while (ws.events.size() <= idx) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        ws.events.push_back(e);
+    }
+    *out = ws.events[idx];
+    return SPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* spt_last_error(void) { return g_last_error.c_str(); }
+const char* spt_version(void) { return "spt-mi355x 0.1 (gfx950 wavefront path tracer)"; }
+
+spt_status spt_init(int32_t device) {
+    spt_status st = ensure_device();
+    if (st) return st;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipFree(nullptr));  // create the context now, not in the first timed call
+    return SPT_OK;
+}
+
+void spt_default_params(spt_render_params* p) {
+    std::memset(p, 0, sizeof(*p));
+    p->width = 512; p->height = 512; p->spp = 100; p->max_depth = 2;  // main.cpp:357-361
+    const float from[3] = {0.0f, 3.03f, 5.0f}, at[3] = {0.0f, 0.03f, 0.0f}, up[3] = {0.0f, 1.0f, 0.0f};
+    std::memcpy(p->camera.look_from, from, sizeof(from));               // main.cpp:383
+    std::memcpy(p->camera.look_at, at, sizeof(at));
+    std::memcpy(p->camera.up, up, sizeof(up));
+    p->camera.lens_radius = 0.0f;
+    p->camera.focal_dist = 1.0f;
+    p->camera.fov_y = 40.0f / 180.0f * (float)M_PI;
+    p->camera.film_size_y = 0.035f;                                    // pinhole.h:11
+    p->tile_index = 0; p->tile_count = 1; p->rows_per_group = 1;
+    p->paths_per_pixel = 0;
+    p->rr_start_depth = 1;
+    p->rng_order = SPT_RNG_Y_FIRST;
+    p->rng_initstate = kPcgDefaultState;
+    p->env[0] = p->env[1] = p->env[2] = 1.0f;
+    p->flags = 0;
+}
+
+uint32_t spt_tile_rows(uint32_t height, uint32_t tile_index, uint32_t tile_count, uint32_t rows_per_group,
+                       uint32_t* rows, uint32_t cap) {
+    if (tile_count == 0 || rows_per_group == 0 || tile_index >= tile_count) return 0;
+    uint32_t n = 0;
+    for (uint32_t r = 0; r < height; r++) {
+        if ((r / rows_per_group) % tile_count != tile_index) continue;
+        if (rows && n < cap) rows[n] = r;
+        n++;
+    }
+    return n;
+}
+
+spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                            const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
+                            const float* tc, uint64_t ntc, const int32_t* mat_id, spt_scene* out) {
+    if (!out) return fail(SPT_ERR_INVALID, "spt_scene_create: out is NULL");
+    *out = nullptr;
+    if (ntri > 0 && (!pos_tri || !pos)) return fail(SPT_ERR_INVALID, "spt_scene_create: NULL positions");
+    if (ntri >= kMaxTriangles) return fail(SPT_ERR_LIMIT, "spt_scene_create: %llu triangles exceeds 2^28", (unsigned long long)ntri);
+    if (nrm_tri && !nrm && nnrm) return fail(SPT_ERR_INVALID, "spt_scene_create: normal indices without normals");
+    spt_status st = ensure_device();
+    if (st) return st;
+    const double t0 = now_ms();
+    std::vector<float> tv((size_t)ntri * 9);
+    for (uint64_t t = 0; t < ntri; t++) {
+        for (int k = 0; k < 3; k++) {
+            int64_t pi = pos_tri[t * 3 + k];
+            if (pi < 0 || (uint64_t)pi >= nvert)
+                return fail(SPT_ERR_INVALID, "spt_scene_create: triangle %llu position index %lld out of range [0,%llu)",
+                            (unsigned long long)t, (long long)pi, (unsigned long long)nvert);
+            for (int c = 0; c < 3; c++) tv[t * 9 + k * 3 + c] = pos[pi * 3 + c];
+        }
+        if (nrm_tri)
+            for (int k = 0; k < 3; k++) {
+                int64_t ni = nrm_tri[t * 3 + k];
+                if (ni < -1 || (ni >= 0 && (uint64_t)ni >= nnrm))
+                    return fail(SPT_ERR_INVALID, "spt_scene_create: triangle %llu normal index %lld out of range",
+                                (unsigned long long)t, (long long)ni);
+            }
+        if (tc_tri && tc)
+            for (int k = 0; k < 3; k++) {
+                int64_t ti = tc_tri[t * 3 + k];
+                if (ti < -1 || (ti >= 0 && (uint64_t)ti >= ntc))
+                    return fail(SPT_ERR_INVALID, "spt_scene_create: triangle %llu texcoord index %lld out of range",
+                                (unsigned long long)t, (long long)ti);
+            }
+    }
+    BvhBuildResult bvh = build_bvh(tv.data(), ntri);
+    const double t1 = now_ms();
+
+    // Slot-ordered device arrays.
+    std::vector<float4> h_tris((size_t)ntri * 3), h_snrm((size_t)ntri * 3);
+    std::vector<float> h_tc(tc_tri && tc ? (size_t)ntri * 6 : 0);
+    std::vector<int32_t> h_o2s((size_t)ntri);
+    for (uint64_t s = 0; s < ntri; s++) {
+        const uint32_t t = bvh.slot2tri[s];
+        h_o2s[t] = (int32_t)s;
+        const float* v = &tv[(size_t)t * 9];
+        for (int k = 0; k < 3; k++) {
+            float w = 0.0f;
+            if (k == 0) { uint32_t id = t; std::memcpy(&w, &id, 4); }
+            h_tris[s * 3 + k] = make_float4(v[k * 3], v[k * 3 + 1], v[k * 3 + 2], w);
+        }
+        // Geometric normal fallback for a missing vertex normal (index -1).
+        V3 g = normalize(cross(v3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), v3(v[6] - v[0], v[7] - v[1], v[8] - v[2])));
+        int32_t mat = mat_id ? mat_id[t] : 0;
+        for (int k = 0; k < 3; k++) {
+            int64_t ni = nrm_tri ? nrm_tri[t * 3 + k] : -1;
+            V3 n = ni >= 0 ? v3(nrm[ni * 3], nrm[ni * 3 + 1], nrm[ni * 3 + 2]) : g;
+            float w = 0.0f;
+            if (k == 0) std::memcpy(&w, &mat, 4);
+            h_snrm[s * 3 + k] = make_float4(n.x, n.y, n.z, w);
+        }
+        if (!h_tc.empty())
+            for (int k = 0; k < 3; k++) {
+                int64_t ti = tc_tri[t * 3 + k];
+                h_tc[s * 6 + k * 2] = ti >= 0 ? tc[ti * 2] : 0.0f;
+                h_tc[s * 6 + k * 2 + 1] = ti >= 0 ? tc[ti * 2 + 1] : 0.0f;
+            }
+    }
+
+    spt_scene_t* sc = new spt_scene_t();
+    (void)hipGetDevice(&sc->device);
+    sc->ntri = ntri;
+    sc->stack_depth = std::max<uint32_t>(1, bvh.max_depth + 1);
+    const float one[3] = {1.0f, 1.0f, 1.0f};
+    spt_status us = SPT_OK;
+    if (!us) us = upload(&sc->nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+    if (!us) us = upload(&sc->tris, h_tris.data(), h_tris.size() * sizeof(float4));
+    if (!us) us = upload(&sc->snrm, h_snrm.data(), h_snrm.size() * sizeof(float4));
+    if (!us) us = upload(&sc->tc, h_tc.data(), h_tc.size() * sizeof(float));
+    if (!us) us = upload(&sc->orig2slot, h_o2s.data(), h_o2s.size() * sizeof(int32_t));
+    if (!us) us = upload(&sc->albedo, one, sizeof(one));
+    if (us) {
+        sc->release();
+        delete sc;
+        return us;
+    }
+    sc->nmat = 1;
+    spt_scene_stats& ss = sc->stats;
+    ss.ntri = ntri;
+    ss.nodes = bvh.nodes.size() / 16;
+    ss.leaves = bvh.leaves;
+    ss.max_depth = bvh.max_depth;
+    ss.max_leaf = bvh.max_leaf;
+    ss.device_bytes = bvh.nodes.size() * 4 + (h_tris.size() + h_snrm.size()) * 16 + h_tc.size() * 4 + h_o2s.size() * 4;
+    ss.build_ms = t1 - t0;
+    ss.sah_cost = bvh.sah_cost;
+    *out = sc;
+    return SPT_OK;
+}
+
+spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t nmat) {
+    if (!sc || !albedo_rgb || nmat == 0) return fail(SPT_ERR_INVALID, "spt_scene_set_albedo: bad arguments");
+    float* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, sizeof(float) * 3 * nmat));
+    HIP_TRY(hipMemcpy(d, albedo_rgb, sizeof(float) * 3 * nmat, hipMemcpyHostToDevice));
+    hfree(sc->albedo);
+    sc->albedo = d;
+    sc->nmat = nmat;
+    return SPT_OK;
+}
+
+spt_status spt_scene_get_stats(spt_scene sc, spt_scene_stats* out) {
+    if (!sc || !out) return fail(SPT_ERR_INVALID, "spt_scene_get_stats: NULL argument");
+    *out = sc->stats;
+    return SPT_OK;
+}
+
+spt_status spt_scene_destroy(spt_scene sc) {
+    if (!sc) return SPT_OK;
+    sc->release();
+    delete sc;
+    return SPT_OK;
+}
+
+spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask, uint32_t mask_size,
+                         const spt_hits* hits, uint32_t n, int32_t do_closest, void* stream) {
+    if (!sc || !rays || !hits) return fail(SPT_ERR_INVALID, "spt_intersect: NULL argument");
+    if (n == 0) return SPT_OK;
+    if (!rays->ox || !rays->oy || !rays->oz || !rays->dx || !rays->dy || !rays->dz)
+        return fail(SPT_ERR_INVALID, "spt_intersect: NULL ray plane");
+    if (!hits->tri_id || !hits->t || !hits->u || !hits->v) return fail(SPT_ERR_INVALID, "spt_intersect: NULL hit plane");
+    if (mask && mask_size != 1 && mask_size != n)
+        return fail(SPT_ERR_INVALID, "spt_intersect: mask_size %u must be 1 or n=%u", mask_size, n);
+    IsectPublicArgs a;
+    a.sc = sc->dev();
+    a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
+    a.dx = rays->dx; a.dy = rays->dy; a.dz = rays->dz;
+    a.tmin = rays->tmin; a.tmax = rays->tmax;
+    a.mask = mask; a.mask_size = mask_size;
+    a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
+    a.n = n;
+    a.closest = do_closest;
+    HIP_TRY(launch_isect_public(a, (hipStream_t)stream));
+    return SPT_OK;
+}
+
+spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hits* hits, const uint8_t* mask,
+                                uint32_t mask_size, uint32_t n, const spt_hit_info* out, void* stream) {
+    if (!sc || !rays || !hits || !out) return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL argument");
+    if (n == 0) return SPT_OK;
+    if (mask && mask_size != 1 && mask_size != n)
+        return fail(SPT_ERR_INVALID, "spt_hit_info_compute: mask_size %u must be 1 or n=%u", mask_size, n);
+    if (sc->ntri == 0) return SPT_OK;
+    HitInfoArgs a;
+    a.sc = sc->dev();
+    a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
+    a.dx = rays->dx; a.dy = rays->dy; a.dz = rays->dz;
+    a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
+    a.mask = mask; a.mask_size = mask_size; a.n = n;
+    a.px = out->px; a.py = out->py; a.pz = out->pz;
+    a.gnx = out->gnx; a.gny = out->gny; a.gnz = out->gnz;
+    a.snx = out->snx; a.sny = out->sny; a.snz = out->snz;
+    a.tcu = out->tcu; a.tcv = out->tcv;
+    a.mat_id = out->mat_id;
+    HIP_TRY(launch_hit_info(a, (hipStream_t)stream));
+    return SPT_OK;
+}
+
+spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev, spt_render_stats* stats_out,
+                      void* stream_) {
+    const double wall0 = now_ms();
+    if (!sc || !pp || !film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL argument");
+    const spt_render_params& p = *pp;
+    if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
+        return fail(SPT_ERR_INVALID, "spt_render: width/height/spp/max_depth must be > 0");
+    if (p.max_depth > kMaxDepthCasts) return fail(SPT_ERR_LIMIT, "spt_render: max_depth %u > %u", p.max_depth, kMaxDepthCasts);
+    if (p.spp >= (1u << 24)) return fail(SPT_ERR_LIMIT, "spt_render: spp must be < 2^24");
+    if ((uint64_t)p.width * p.height >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: image too large");
+    if (p.tile_count == 0 || p.rows_per_group == 0 || p.tile_index >= p.tile_count)
+        return fail(SPT_ERR_INVALID, "spt_render: bad tile (%u of %u, %u rows/group)", p.tile_index, p.tile_count,
+                    p.rows_per_group);
+    if (p.rng_order > 1) return fail(SPT_ERR_INVALID, "spt_render: rng_order must be 0 or 1");
+    hipStream_t stream = (hipStream_t)stream_;
+    const uint32_t rows = spt_tile_rows(p.height, p.tile_index, p.tile_count, p.rows_per_group, nullptr, 0);
+    const uint64_t P = (uint64_t)rows * p.width;
+    spt_render_stats rs{};
+    rs.tile_rows = rows;
+    rs.paths = P * p.spp;
+    if (P == 0) {
+        if (stats_out) *stats_out = rs;
+        return SPT_OK;
+    }
+    // Paths in flight: enough lanes to fill 256 CUs (~1M) but at most spp per pixel.
+    uint64_t k = p.paths_per_pixel;
+    if (k == 0) {
+        const uint64_t target = 1ull << 20;
+        k = (target + P - 1) / P;
+    }
+    k = std::max<uint64_t>(1, std::min<uint64_t>(k, p.spp));
+    const uint64_t C = P * k;
+    if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: %llu paths in flight exceeds 2^31", (unsigned long long)C);
+    rs.paths_in_flight = (uint32_t)C;
+    spt_status st = ensure_workspace(sc->ws, C, (size_t)k * 3 * P);
+    if (st) return st;
+    Workspace& ws = sc->ws;
+    const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
+
+    const Camera cam = make_camera(p);
+    PathQueue qa = carve_queue(ws.qa, ws.cap), qb = carve_queue(ws.qb, ws.cap);
+    int32_t* hit_slot = (int32_t*)ws.hits;
+    float* hit_t = (float*)(hit_slot + ws.cap);
+    float* hit_u = hit_t + ws.cap;
+    float* hit_v = hit_u + ws.cap;
+
+    HIP_TRY(hipMemsetAsync(ws.film, 0, sizeof(float) * k * 3 * P, stream));
+    HIP_TRY(hipMemsetAsync(ws.counts, 0, 64, stream));
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ws.counts, (int)C, 1, stream));
+
+    size_t ev = 0;
+    hipEvent_t e0, e1;
+    if (timing) {
+        if ((st = get_event(ws, ev++, &e0))) return st;
+        HIP_TRY(hipEventRecord(e0, stream));
+    }
+    CameraInitArgs ca;
+    ca.q = qa; ca.cam = cam; ca.P = (uint32_t)P; ca.W = p.width; ca.k_eff = (uint32_t)k;
+    ca.max_depth = p.max_depth; ca.rng_order = p.rng_order;
+    ca.tile_index = p.tile_index; ca.tile_count = p.tile_count; ca.rows_per_group = p.rows_per_group;
+    ca.initstate = p.rng_initstate;
+    HIP_TRY(launch_camera_init(ca, (uint32_t)C, stream));
+    if (timing) {
+        if ((st = get_event(ws, ev++, &e1))) return st;
+        HIP_TRY(hipEventRecord(e1, stream));
+    }
+    std::vector<std::pair<size_t, int>> timed;  // (event index of start, kind 0 cam 1 isect 2 shade 3 resolve)
+    if (timing) timed.push_back({0, 0});
+
+    IsectQueueArgs ia;
+    ia.sc = sc->dev();
+    ia.hit_slot = hit_slot; ia.hit_t = hit_t; ia.hit_u = hit_u; ia.hit_v = hit_v;
+    ia.max_depth = p.max_depth;
+    ShadeArgs sa;
+    sa.sc = sc->dev();
+    sa.hit_slot = hit_slot; sa.hit_t = hit_t; sa.hit_u = hit_u; sa.hit_v = hit_v;
+    sa.film = ws.film;
+    sa.stats = ws.stats;
+    sa.cam = cam;
+    sa.P = (uint32_t)P; sa.W = p.width; sa.k = (uint32_t)k; sa.spp = p.spp; sa.max_depth = p.max_depth;
+    sa.rr_start = p.rr_start_depth; sa.rng_order = p.rng_order;
+    sa.tile_index = p.tile_index; sa.tile_count = p.tile_count; sa.rows_per_group = p.rows_per_group;
+    sa.env_r = p.env[0]; sa.env_g = p.env[1]; sa.env_b = p.env[2];
+    const uint64_t per_sample = 4ull + 2ull * p.max_depth;
+    for (uint32_t pairs = 0; pairs <= p.max_depth; pairs++)
+        sa.jumps[pairs] = pcg_jump_coeffs(2ull * (p.max_depth - pairs) + (k - 1) * per_sample);
+
+    // Iterate isect -> shade until the queue drains.  The live count never
+    // grows, so a stale (larger) host copy is a safe grid size; it is read
+    // back once per batch, pipelined one batch behind the launches.
+    const uint64_t max_iters = ((uint64_t)p.spp + k - 1) / k * p.max_depth + 4ull * p.max_depth + 64;
+    uint32_t known = (uint32_t)C;
+    uint64_t iters = 0;
+    int cur = 0;
+    int pending = -1;
+    uint32_t batch = 4, nbatch = 0;
+    while (true) {
+        for (uint32_t b = 0; b < batch; b++) {
+            PathQueue& qin = cur == 0 ? qa : qb;
+            PathQueue& qout = cur == 0 ? qb : qa;
+            ia.q = qin;
+            ia.count = ws.counts + cur;
+            if (timing) {
+                if ((st = get_event(ws, ev, &e0))) return st;
+                HIP_TRY(hipEventRecord(e0, stream));
+                timed.push_back({ev, 1});
+                ev += 2;
+            }
+            HIP_TRY(launch_isect_queue(ia, known, stream));
+            if (timing) {
+                if ((st = get_event(ws, ev - 1, &e1))) return st;
+                HIP_TRY(hipEventRecord(e1, stream));
+            }
+            HIP_TRY(hipMemsetAsync(ws.counts + (1 - cur), 0, sizeof(uint32_t), stream));
+            sa.in = qin; sa.out = qout;
+            sa.count_in = ws.counts + cur;
+            sa.count_out = ws.counts + (1 - cur);
+            if (timing) {
+                if ((st = get_event(ws, ev, &e0))) return st;
+                HIP_TRY(hipEventRecord(e0, stream));
+                timed.push_back({ev, 2});
+                ev += 2;
+            }
+            HIP_TRY(launch_shade(sa, known, stream));
+            if (timing) {
+                if ((st = get_event(ws, ev - 1, &e1))) return st;
+                HIP_TRY(hipEventRecord(e1, stream));
+            }
+            cur = 1 - cur;
+            iters++;
+        }
+        const int slot = (int)(nbatch++ & 1u);
+        HIP_TRY(hipMemcpyAsync(ws.host_counts + slot, ws.counts + cur, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipEventRecord(ws.count_ev[slot], stream));
+        if (pending >= 0) {
+            HIP_TRY(hipEventSynchronize(ws.count_ev[pending]));
+            known = ws.host_counts[pending];
+            if (known == 0) break;
+        }
+        pending = slot;
+        if (iters > max_iters)
+            return fail(SPT_ERR_HIP, "spt_render: queue did not drain after %llu iterations", (unsigned long long)iters);
+        batch = std::min<uint32_t>(batch * 2, 16);
+    }
+
+    if (timing) {
+        if ((st = get_event(ws, ev, &e0))) return st;
+        HIP_TRY(hipEventRecord(e0, stream));
+        timed.push_back({ev, 3});
+        ev += 2;
+    }
+    HIP_TRY(launch_resolve(ws.film, film_dev, (uint32_t)P, (uint32_t)k, p.spp, stream));
+    if (timing) {
+        if ((st = get_event(ws, ev - 1, &e1))) return st;
+        HIP_TRY(hipEventRecord(e1, stream));
+    }
+    unsigned long long hstats[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(hstats, ws.stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    rs.ray_casts = hstats[0];
+    rs.continuations = hstats[1];
+    rs.regenerations = hstats[2];
+    rs.iterations = iters;
+    if (timing) {
+        for (auto& tk : timed) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, ws.events[tk.first], ws.events[tk.first + 1]));
+            if (tk.second == 0) rs.camera_ms += ms;
+            else if (tk.second == 1) rs.isect_ms += ms;
+            else if (tk.second == 2) rs.shade_ms += ms;
+            else rs.resolve_ms += ms;
+        }
+    }
+    rs.total_ms = now_ms() - wall0;
+    if (stats_out) *stats_out = rs;
+    return SPT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,395 @@
+// kernels.hip — the hot path on gfx950: BVH traversal (isect), Lambertian
+// shade + sample + Russian roulette with wave-ballot compaction and path
+// regeneration (shade), camera generation and film resolve.
+//
+// Replaces wavefront_isect.cu:36-112 (OptiX raygen / closest-hit / miss) and
+// the Enoki-JIT bounce loop body main.cpp:385-426.
+#include "spt_internal.h"
+
+namespace spt {
+
+// ------------------------------------------------------------- traversal
+struct TraceHit {
+    int32_t slot;
+    uint32_t id;
+    float t, u, v;
+};
+
+// Stack-based BVH2 traversal, near child first, stack in LDS at
+// stk[i * kIsectBlock] (lane-interleaved: conflict-free, one bank per lane).
+// Closest hit: smallest t, ties broken toward the smaller original triangle
+// id so the answer does not depend on the tree.  anyhit: stop at the first
+// accepted triangle (OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
+__device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
+                                          bool anyhit, uint32_t* __restrict__ stk) {
+    TraceHit h;
+    h.slot = -1;
+    h.id = 0xffffffffu;
+    h.t = tmax;
+    h.u = 0.0f;
+    h.v = 0.0f;
+    if (sc.empty) return h;
+    const WoopRay wr = woop_setup(o, d);
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float4* __restrict__ nodes = sc.nodes;
+    const float4* __restrict__ tris = sc.tris;
+    int32_t node = 0;
+    uint32_t sp = 0;
+    while (true) {
+        if (node >= 0) {
+            const float4* np = nodes + (size_t)node * 4;
+            const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
+            const float a0 = (n0.x - o.x) * ix, a1 = (n0.y - o.x) * ix;
+            const float b0 = (n0.z - o.y) * iy, b1 = (n0.w - o.y) * iy;
+            const float c0 = (n2.x - o.z) * iz, c1 = (n2.y - o.z) * iz;
+            const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), tmin));
+            const float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1)) * kBoxPad;
+            const float d0 = (n1.x - o.x) * ix, d1 = (n1.y - o.x) * ix;
+            const float e0 = (n1.z - o.y) * iy, e1 = (n1.w - o.y) * iy;
+            const float f0 = (n2.z - o.z) * iz, f1 = (n2.w - o.z) * iz;
+            const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fmaxf(fminf(f0, f1), tmin));
+            const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1)) * kBoxPad;
+            const bool h0 = tn0 <= fminf(tf0, h.t);
+            const bool h1 = tn1 <= fminf(tf1, h.t);
+            const int32_t ch0 = (int32_t)f2u(n3.x), ch1 = (int32_t)f2u(n3.y);
+            if (h0 && h1) {
+                const bool swp = tn1 < tn0;
+                stk[sp * kIsectBlock] = (uint32_t)(swp ? ch0 : ch1);
+                sp++;
+                node = swp ? ch1 : ch0;
+            } else if (h0) {
+                node = ch0;
+            } else if (h1) {
+                node = ch1;
+            } else {
+                if (sp == 0) break;
+                sp--;
+                node = (int32_t)stk[sp * kIsectBlock];
+            }
+        } else {
+            const uint32_t code = ~(uint32_t)node;
+            const uint32_t first = code >> 3, cnt = (code & 7u) + 1u;
+            for (uint32_t i = 0; i < cnt; i++) {
+                const uint32_t s = first + i;
+                const float4 t0 = tris[(size_t)s * 3], t1 = tris[(size_t)s * 3 + 1], t2 = tris[(size_t)s * 3 + 2];
+                float t, u, v;
+                if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), tmin, h.t, t,
+                              u, v)) {
+                    const uint32_t id = f2u(t0.w);
+                    if (t < h.t || id < h.id) {
+                        h.t = t;
+                        h.id = id;
+                        h.slot = (int32_t)s;
+                        h.u = u;
+                        h.v = v;
+                    }
+                }
+            }
+            if (anyhit && h.slot >= 0) break;
+            if (sp == 0) break;
+            sp--;
+            node = (int32_t)stk[sp * kIsectBlock];
+        }
+    }
+    return h;
+}
+
+// Wavefront isect over the path queue: one lane per queued ray.  The last
+// cast of a path only needs a yes/no answer (a miss is the only thing that
+// contributes, main.cpp:407), so it runs as an any-hit query.
+__global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs a) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
+    const uint32_t n = *a.count;
+    if (i >= n) return;
+    const V3 o = v3(a.q.ox[i], a.q.oy[i], a.q.oz[i]);
+    const V3 d = v3(a.q.dx[i], a.q.dy[i], a.q.dz[i]);
+    const uint32_t depth = a.q.meta[i] & ((1u << kMetaDepthBits) - 1u);
+    const bool anyhit = depth + 1 >= a.max_depth;
+    const TraceHit h = trace(a.sc, o, d, kRayTmin, kRayTmax, anyhit, lds_stack + threadIdx.x);
+    a.hit_slot[i] = h.slot;
+    a.hit_t[i] = h.t;
+    a.hit_u[i] = h.u;
+    a.hit_v[i] = h.v;
+}
+
+// __raygen__rg (wavefront_isect.cu:80-112) semantics for the public C ABI.
+__global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicArgs a) {
+    extern __shared__ uint32_t lds_stack[];
+    const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const bool m = !a.mask || ((a.mask_size == 1) ? (a.mask[0] != 0) : (a.mask[i] != 0));
+    if (!m) return;
+    const V3 o = v3(a.ox[i], a.oy[i], a.oz[i]);
+    const V3 d = v3(a.dx[i], a.dy[i], a.dz[i]);
+    const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
+    const TraceHit h = trace(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x);
+    if (h.slot < 0) {
+        a.tri_id[i] = -1;
+        return;
+    }
+    a.tri_id[i] = (int32_t)h.id;
+    a.t[i] = h.t;
+    a.u[i] = h.u;
+    a.v[i] = h.v;
+}
+
+// ------------------------------------------------------------ camera gen
+__device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32_t order, uint32_t x,
+                                           uint32_t y, V3& o, V3& d) {
+    float xi_x, xi_y;
+    draw2(rng, order, xi_x, xi_y);              // main.cpp:395
+    o = camera_sample_pos(cam, xi_x, xi_y);
+    draw2(rng, order, xi_x, xi_y);              // main.cpp:396
+    d = camera_sample_dir(cam, x, y, o, xi_x, xi_y);
+}
+
+__device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix,
+                                           uint32_t meta, uint64_t rng, float tr, float tg, float tb) {
+    q.ox[j] = o.x; q.oy[j] = o.y; q.oz[j] = o.z;
+    q.dx[j] = d.x; q.dy[j] = d.y; q.dz[j] = d.z;
+    q.pix[j] = pix;
+    q.meta[j] = meta;
+    q.rng[j] = rng;
+    q.tr[j] = tr; q.tg[j] = tg; q.tb[j] = tb;
+}
+
+// Entry e = s * P + p starts sample s of tile pixel p (s < k_eff).
+__global__ __launch_bounds__(256) void camera_init_kernel(CameraInitArgs a, uint32_t items) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= items) return;
+    const uint32_t s = e / a.P, p = e % a.P;
+    const uint32_t lx = p % a.W, ly = p / a.W;
+    const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
+    const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
+    Pcg32 rng;
+    rng.seed(a.initstate, (uint64_t)gpix);                   // main.cpp:376
+    if (s) rng.state = pcg_apply(pcg_jump_coeffs((uint64_t)s * (4u + 2u * a.max_depth)), rng.state, rng.inc);
+    V3 o, d;
+    camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
+    store_path(a.q, e, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f);
+}
+
+// ----------------------------------------------------------------- shade
+// main.cpp:404-425 for one cast of every queued path, plus path regeneration
+// (a finished sample immediately starts the pixel's next sample in the same
+// lane) and ballot/mbcnt compaction of the survivors into the out queue
+// (one atomic per block).
+__global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
+    __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
+    __shared__ uint32_t s_wave_off[kShadeBlock / 64];
+    __shared__ uint32_t s_stats[3];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t i = blockIdx.x * kShadeBlock + tid;
+    const uint32_t n = *a.count_in;
+    if (tid < 3) s_stats[tid] = 0;
+    __syncthreads();
+
+    bool emit = false, cont = false, regen = false;
+    V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
+    uint32_t pix = 0, nmeta = 0;
+    uint64_t nrng = 0;
+    float tr = 1.0f, tg = 1.0f, tb = 1.0f;
+    if (i < n) {
+        pix = a.in.pix[i];
+        const uint32_t meta = a.in.meta[i];
+        const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
+        const uint32_t sample = meta >> kMetaDepthBits;
+        const int32_t slot = a.hit_slot[i];
+        tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
+        const uint32_t lx = pix % a.W, ly = pix / a.W;
+        const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
+        const uint32_t gpix = gy * a.W + lx;
+        Pcg32 rng;
+        rng.state = a.in.rng[i];
+        rng.inc = ((uint64_t)gpix << 1u) | 1u;
+        bool term = true;
+        uint32_t pairs = depth;  // scatter draw pairs consumed by this sample
+        if (slot < 0) {
+            // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
+            const uint32_t fs = sample % a.k;
+            float* f = a.film + (size_t)fs * 3 * a.P + pix;
+            f[0] = f[0] + tr * a.env_r;
+            f[(size_t)a.P] = f[(size_t)a.P] + tg * a.env_g;
+            f[(size_t)2 * a.P] = f[(size_t)2 * a.P] + tb * a.env_b;
+        } else if (depth + 1 < a.max_depth) {
+            const V3 o = v3(a.in.ox[i], a.in.oy[i], a.in.oz[i]);
+            const V3 d = v3(a.in.dx[i], a.in.dy[i], a.in.dz[i]);
+            const float t = a.hit_t[i], u = a.hit_u[i], v = a.hit_v[i];
+            float xi_x, xi_y;
+            draw2(rng, a.rng_order, xi_x, xi_y);               // main.cpp:413
+            pairs = depth + 1;
+            const float4 m0 = a.sc.snrm[(size_t)slot * 3];
+            const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
+            const float4 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+            const float w = (1.0f - u) - v;                      // add_math.h:6
+            const V3 sn = v3((w * m0.x + u * m1.x) + v * m2.x,  // optix_backend.h:483-484
+                             (w * m0.y + u * m1.y) + v * m2.y,
+                             (w * m0.z + u * m1.z) + v * m2.z);
+            const V3 hp = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);  // optix_backend.h:469
+            const Frame fr = frame_from_normal(sn);              // main.cpp:414
+            const V3 out = to_world(fr, cosine_hemisphere(xi_x, xi_y));  // main.cpp:418-419
+            uint32_t mat = f2u(m0.w);
+            if (mat >= a.sc.nmat) mat = 0;
+            tr = tr * a.sc.albedo[mat * 3];                      // main.cpp:422
+            tg = tg * a.sc.albedo[mat * 3 + 1];
+            tb = tb * a.sc.albedo[mat * 3 + 2];
+            term = false;
+            if (depth + 1 >= a.rr_start) {
+                const float q = fmaxf(tr, fmaxf(tg, tb));
+                if (q < 1.0f) {
+                    if (rr_uniform(gpix, sample, depth) >= q) {
+                        term = true;
+                    } else {
+                        tr = tr / q; tg = tg / q; tb = tb / q;
+                    }
+                }
+            }
+            if (!term) {
+                emit = cont = true;
+                no = hp;                                          // main.cpp:423
+                nd = out;                                         // main.cpp:424
+                nmeta = meta + 1u;
+                nrng = rng.state;
+            }
+        }
+        // else: hit on the last cast — the path ends without contribution.
+        if (term) {
+            const uint32_t next = sample + a.k;
+            if (next < a.spp) {
+                rng.state = pcg_apply(a.jumps[pairs], rng.state, rng.inc);
+                camera_ray(a.cam, rng, a.rng_order, lx, gy, no, nd);
+                emit = regen = true;
+                nmeta = next << kMetaDepthBits;
+                nrng = rng.state;
+                tr = tg = tb = 1.0f;                              // main.cpp:391
+            }
+        }
+    }
+
+    // Compaction: wave ballot + mbcnt rank, one atomicAdd per block.
+    const uint64_t ball = __ballot(emit);
+    const uint32_t rank =
+        __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
+    const uint64_t bc = __ballot(cont), br = __ballot(regen), bi = __ballot(i < n);
+    if (lane == 0) {
+        s_wave_cnt[wave] = (uint32_t)__popcll(ball);
+        atomicAdd(&s_stats[0], (uint32_t)__popcll(bi));
+        atomicAdd(&s_stats[1], (uint32_t)__popcll(bc));
+        atomicAdd(&s_stats[2], (uint32_t)__popcll(br));
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t total = 0;
+        for (uint32_t w = 0; w < kShadeBlock / 64; w++) {
+            s_wave_off[w] = total;
+            total += s_wave_cnt[w];
+        }
+        const uint32_t base = total ? atomicAdd(a.count_out, total) : 0u;
+        for (uint32_t w = 0; w < kShadeBlock / 64; w++) s_wave_off[w] += base;
+        if (s_stats[0]) {
+            atomicAdd(&a.stats[0], (unsigned long long)s_stats[0]);
+            if (s_stats[1]) atomicAdd(&a.stats[1], (unsigned long long)s_stats[1]);
+            if (s_stats[2]) atomicAdd(&a.stats[2], (unsigned long long)s_stats[2]);
+        }
+    }
+    __syncthreads();
+    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb);
+}
+
+// film[k][3][P] -> out[3][P] / spp  (main.cpp:429)
+__global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ film, float* __restrict__ out,
+                                                      uint32_t P, uint32_t k_eff, uint32_t spp) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    for (uint32_t c = 0; c < 3; c++) {
+        float sum = 0.0f;
+        for (uint32_t s = 0; s < k_eff; s++) sum = sum + film[((size_t)s * 3 + c) * P + p];
+        out[(size_t)c * P + p] = sum / (float)spp;
+    }
+}
+
+// optix_backend.h:462-486 + main.cpp:325 for the public ABI.
+__global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const bool m = !a.mask || ((a.mask_size == 1) ? (a.mask[0] != 0) : (a.mask[i] != 0));
+    const int32_t id = a.tri_id[i];
+    if (!m || id < 0) return;                                    // active = neq(tri_id,-1) && mask
+    const int32_t slot = a.sc.orig2slot[id];
+    const float t = a.t[i], u = a.u[i], v = a.v[i];
+    if (a.px) {
+        a.px[i] = a.ox[i] + t * a.dx[i];
+        a.py[i] = a.oy[i] + t * a.dy[i];
+        a.pz[i] = a.oz[i] + t * a.dz[i];
+    }
+    if (a.gnx) {
+        const float4 p0 = a.sc.tris[(size_t)slot * 3], p1 = a.sc.tris[(size_t)slot * 3 + 1],
+                     p2 = a.sc.tris[(size_t)slot * 3 + 2];
+        const V3 g = normalize(cross(v3(p1.x - p0.x, p1.y - p0.y, p1.z - p0.z),  // add_math.h:9-16
+                                     v3(p2.x - p0.x, p2.y - p0.y, p2.z - p0.z)));
+        a.gnx[i] = g.x; a.gny[i] = g.y; a.gnz[i] = g.z;
+    }
+    const float w = (1.0f - u) - v;
+    const float4 m0 = a.sc.snrm[(size_t)slot * 3];
+    if (a.snx) {
+        const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1], m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+        a.snx[i] = (w * m0.x + u * m1.x) + v * m2.x;
+        a.sny[i] = (w * m0.y + u * m1.y) + v * m2.y;
+        a.snz[i] = (w * m0.z + u * m1.z) + v * m2.z;
+    }
+    if (a.tcu) {
+        float cu = 0.0f, cv = 0.0f;
+        if (a.sc.tc) {
+            const float* c = a.sc.tc + (size_t)slot * 6;
+            cu = (w * c[0] + u * c[2]) + v * c[4];
+            cv = (w * c[1] + u * c[3]) + v * c[5];
+        }
+        a.tcu[i] = cu;
+        a.tcv[i] = cv;
+    }
+    if (a.mat_id) a.mat_id[i] = (int32_t)f2u(m0.w);
+}
+
+// ------------------------------------------------------------- launchers
+static inline uint32_t blocks_for(uint32_t items, uint32_t block) { return (items + block - 1) / block; }
+
+hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+    if (grid_items == 0) return hipSuccess;
+    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
+    hipLaunchKernelGGL(isect_queue_kernel, dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
+    hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s) {
+    if (grid_items == 0) return hipSuccess;
+    hipLaunchKernelGGL(shade_kernel, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_camera_init(const CameraInitArgs& a, uint32_t items, hipStream_t s) {
+    if (items == 0) return hipSuccess;
+    hipLaunchKernelGGL(camera_init_kernel, dim3(blocks_for(items, 256)), dim3(256), 0, s, a, items);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve(const float* film, float* out, uint32_t P, uint32_t k_eff, uint32_t spp, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(resolve_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, film, out, P, k_eff, spp);
+    return hipGetLastError();
+}
+
+hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(hit_info_kernel, dim3(blocks_for(a.n, 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace spt

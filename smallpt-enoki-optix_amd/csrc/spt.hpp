@@ -1,0 +1,56 @@
+// spt.hpp — C++ host wrapper over include/spt.h keeping the reference's
+// exception convention (OPTIX_CHECK / CUDA_CHECK throw std::runtime_error,
+// optix_backend.h:25-66) and its Scene / backend call shape
+// (Scene::add_triangle_mesh / commit / intersect, main.cpp:286-352).
+#pragma once
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/spt.h"
+
+namespace spt {
+
+inline void check(spt_status s, const char* what) {
+    if (s != SPT_OK) throw std::runtime_error(std::string(what) + " failed (" + std::to_string(s) + "): " + spt_last_error());
+}
+
+struct Mesh {
+    spt_mesh m{};
+    explicit Mesh(const std::string& path) { check(spt_obj_load(path.c_str(), &m), "spt_obj_load"); }
+    ~Mesh() { spt_mesh_free(&m); }
+    Mesh(const Mesh&) = delete;
+    Mesh& operator=(const Mesh&) = delete;
+};
+
+// main.cpp:286-352 Scene, minus the Enoki arrays: geometry lives on the GPU
+// behind spt_scene.
+class Scene {
+  public:
+    Scene() = default;
+    ~Scene() { if (scene_) spt_scene_destroy(scene_); }
+    Scene(const Scene&) = delete;
+    Scene& operator=(const Scene&) = delete;
+
+    void add_triangle_mesh(const std::string& obj_path) { mesh_.reset(new Mesh(obj_path)); }  // main.cpp:288
+    void commit(int device = 0) {                                                            // main.cpp:312
+        if (!mesh_) throw std::runtime_error("Scene::commit: no mesh added");
+        check(spt_init(device), "spt_init");
+        const spt_mesh& m = mesh_->m;
+        check(spt_scene_create(m.pos_tri, m.pos, m.nvert, m.ntri, m.nrm_tri, m.nrm, m.nnrm, m.tc_tri, m.tc, m.ntc,
+                               m.mat_id, &scene_),
+              "spt_scene_create");
+    }
+    void render(const spt_render_params& p, float* film_dev, spt_render_stats* stats, void* stream = nullptr) {
+        check(spt_render(scene_, &p, film_dev, stats, stream), "spt_render");
+    }
+    spt_scene handle() const { return scene_; }
+    const spt_mesh& mesh() const { return mesh_->m; }
+
+  private:
+    std::unique_ptr<Mesh> mesh_;
+    spt_scene scene_ = nullptr;
+};
+
+}  // namespace spt

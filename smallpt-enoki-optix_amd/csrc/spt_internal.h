@@ -1,0 +1,108 @@
+// spt_internal.h — device-side data layout and kernel launchers (not part of
+// the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spt_math.h"
+
+namespace spt {
+
+constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
+constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
+constexpr uint32_t kShadeBlock = 256;       // shade: 4 waves, one queue atomic per block
+constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
+
+// Path queue, structure of arrays (ray.h layout for the ray planes).
+struct PathQueue {
+    float *ox, *oy, *oz, *dx, *dy, *dz;
+    uint32_t* pix;    // tile-local pixel index
+    uint32_t* meta;   // sample << 8 | cast index
+    uint64_t* rng;    // PCG32 state (inc = 2 * global_pixel + 1)
+    float *tr, *tg, *tb;  // path throughput
+};
+
+// Geometry on device, leaf ("slot") order.
+struct DeviceScene {
+    const float4* nodes;   // 4 per node (bvh_build.h)
+    const float4* tris;    // 3 per slot: v0 (w = original id bits), v1, v2
+    const float4* snrm;    // 3 per slot: n0 (w = material id bits), n1, n2
+    const float* tc;       // 6 per slot (u0 v0 u1 v1 u2 v2) or null
+    const int32_t* orig2slot;
+    const float* albedo;   // 3 per material
+    uint32_t nmat;
+    uint32_t stack_depth;  // LDS stack entries per lane
+    uint32_t empty;        // no triangles
+};
+
+struct IsectQueueArgs {
+    DeviceScene sc;
+    PathQueue q;
+    const uint32_t* count;
+    int32_t* hit_slot;
+    float *hit_t, *hit_u, *hit_v;
+    uint32_t max_depth;
+};
+
+struct IsectPublicArgs {
+    DeviceScene sc;
+    const float *ox, *oy, *oz, *dx, *dy, *dz, *tmin, *tmax;
+    const uint8_t* mask;
+    uint32_t mask_size;
+    int32_t* tri_id;
+    float *t, *u, *v;
+    uint32_t n;
+    int32_t closest;
+};
+
+struct ShadeArgs {
+    DeviceScene sc;
+    PathQueue in, out;
+    const int32_t* hit_slot;
+    const float *hit_t, *hit_u, *hit_v;
+    const uint32_t* count_in;
+    uint32_t* count_out;
+    float* film;              // [k][3][P]
+    unsigned long long* stats; // casts, continuations, regenerations
+    Camera cam;
+    uint32_t P, W, k, spp, max_depth, rr_start, rng_order;
+    uint32_t tile_index, tile_count, rows_per_group;
+    float env_r, env_g, env_b;
+    PcgJump jumps[kMaxDepthCasts + 1];  // indexed by scatter pairs consumed
+};
+
+struct CameraInitArgs {
+    PathQueue q;
+    Camera cam;
+    uint32_t P, W, k_eff, max_depth, rng_order;
+    uint32_t tile_index, tile_count, rows_per_group;
+    uint64_t initstate;
+};
+
+struct HitInfoArgs {
+    DeviceScene sc;
+    const float *ox, *oy, *oz, *dx, *dy, *dz;
+    const int32_t* tri_id;
+    const float *t, *u, *v;
+    const uint8_t* mask;
+    uint32_t mask_size, n;
+    float *px, *py, *pz, *gnx, *gny, *gnz, *snx, *sny, *snz, *tcu, *tcv;
+    int32_t* mat_id;
+};
+
+// Tile-local row -> global row for interleaved row groups.
+SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_t tile_count,
+                                uint32_t rows_per_group) {
+    uint32_t g = local_row / rows_per_group;
+    return (g * tile_count + tile_index) * rows_per_group + local_row % rows_per_group;
+}
+
+hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
+hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
+hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s);
+hipError_t launch_camera_init(const CameraInitArgs& a, uint32_t items, hipStream_t s);
+hipError_t launch_resolve(const float* film, float* out, uint32_t P, uint32_t k_eff, uint32_t spp,
+                          hipStream_t s);
+hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s);
+
+}  // namespace spt

@@ -1,0 +1,240 @@
+// spt_math.h — __host__ __device__ math of the hot path (camera, PCG32,
+// sampling, shading frame, watertight triangle test).  Compiled by hipcc for
+// gfx950 (kernels) and for the host (camera constants, jump tables).
+//
+// Floating point: every translation unit is built with -ffp-contract=off and
+// correctly rounded f32 division/sqrt; every FMA below is an explicit fmaf().
+// The op order of each function is the specification the CPU oracle
+// (oracle/oracle.c) restates independently; parity tests compare bitwise.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SPT_HD __host__ __device__ __forceinline__
+
+namespace spt {
+
+constexpr float kPi = 3.14159265358979323846f;
+constexpr uint64_t kPcgMult = 0x5851f42d4c957f2dULL;
+constexpr uint64_t kPcgDefaultState = 0x853c49e6748fea9bULL;  // main.cpp:376
+constexpr float kRayTmin = 0.001f;                             // ray.h:16
+constexpr float kRayTmax = 1e20f;                              // ray.h:16
+constexpr float kBoxPad = 1.000001f;  // conservative slab exit (Ize 2013 + margin)
+
+SPT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+SPT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// ------------------------------------------------------------------ PCG32
+// Enoki random.h (external): next_uint32 / next_float32; seeded at
+// main.cpp:376 with initseq = pixel index.
+struct Pcg32 {
+    uint64_t state, inc;
+    SPT_HD uint32_t next() {
+        uint64_t old = state;
+        state = old * kPcgMult + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((32u - rot) & 31u));
+    }
+    SPT_HD float next_float() { return u2f((next() >> 9) | 0x3f800000u) - 1.0f; }
+    SPT_HD void seed(uint64_t initstate, uint64_t initseq) {
+        state = 0;
+        inc = (initseq << 1u) | 1u;
+        next();
+        state += initstate;
+        next();
+    }
+};
+
+// Jump-ahead: after n steps, state' = mul * state + add * inc (mod 2^64).
+struct PcgJump { uint64_t mul, add; };
+SPT_HD PcgJump pcg_jump_coeffs(uint64_t n) {
+    uint64_t acc_mul = 1, acc_add = 0, cur_mul = kPcgMult, cur_add = 1;
+    while (n > 0) {
+        if (n & 1) { acc_mul *= cur_mul; acc_add = acc_add * cur_mul + cur_add; }
+        cur_add = (cur_mul + 1) * cur_add;
+        cur_mul *= cur_mul;
+        n >>= 1;
+    }
+    return {acc_mul, acc_add};
+}
+SPT_HD uint64_t pcg_apply(PcgJump j, uint64_t state, uint64_t inc) { return j.mul * state + j.add * inc; }
+
+// Real2C(next(), next()) — argument evaluation order is unspecified in the
+// reference (main.cpp:395,396,413); y-first = first draw to .y.
+SPT_HD void draw2(Pcg32& r, uint32_t order, float& x, float& y) {
+    float a = r.next_float();
+    float b = r.next_float();
+    if (order == 0) { y = a; x = b; } else { x = a; y = b; }
+}
+
+// ------------------------------------------------------------------ sincos
+// Cephes single-precision joint sin/cos (Enoki's sincos; used at mapping.h:9,25).
+SPT_HD void sincos_cephes(float x, float& s_out, float& c_out) {
+    float xa = fabsf(x);
+    int32_t j = (int32_t)(xa * 1.2732395447351626862f);
+    j = (j + 1) & ~1;
+    float y = (float)j;
+    uint32_t sign_sin = (((uint32_t)j << 29) & 0x80000000u) ^ (f2u(x) & 0x80000000u);
+    uint32_t sign_cos = ((uint32_t)(~(j - 2)) << 29) & 0x80000000u;
+    y = ((xa - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    float z = y * y;
+    float s = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z;
+    float c = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f) * z;
+    s = fmaf(s, y, y);
+    c = fmaf(c, z, fmaf(z, -0.5f, 1.0f));
+    bool poly = (j & 2) == 0;
+    float rs = poly ? s : c;
+    float rc = poly ? c : s;
+    s_out = u2f(f2u(rs) ^ sign_sin);
+    c_out = u2f(f2u(rc) ^ sign_cos);
+}
+
+// ------------------------------------------------------------------ vectors
+struct V3 { float x, y, z; };
+SPT_HD V3 v3(float x, float y, float z) { return {x, y, z}; }
+SPT_HD V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+SPT_HD float dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+SPT_HD V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+// Enoki normalize = v * rsqrt(|v|^2), restated as v * (1 / sqrt(|v|^2)).
+SPT_HD V3 normalize(V3 v) {
+    float inv = 1.0f / sqrtf(dot(v, v));
+    return {v.x * inv, v.y * inv, v.z * inv};
+}
+SPT_HD float comp(V3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
+
+// Frame3 (coordframe.h:5-51): columns bx, by, bz; to_world = M * l.
+struct Frame { V3 bx, by, bz; };
+SPT_HD V3 to_world(const Frame& f, V3 l) {
+    return {(f.bx.x * l.x + f.by.x * l.y) + f.bz.x * l.z,
+            (f.bx.y * l.x + f.by.y * l.y) + f.bz.y * l.z,
+            (f.bx.z * l.x + f.by.z * l.y) + f.bz.z * l.z};
+}
+SPT_HD V3 to_local(const Frame& f, V3 w) { return {dot(f.bx, w), dot(f.by, w), dot(f.bz, w)}; }
+// coordframe.h:17-30; the normal is used as given (not renormalised).
+SPT_HD Frame frame_from_normal(V3 n) {
+    float sign = copysignf(1.0f, n.y);
+    float a = -1.0f / (sign + n.y);
+    float b = (n.z * n.x) * a;
+    Frame f;
+    f.bx = {sign + (n.x * n.x) * a, -n.x, b};
+    f.by = n;
+    f.bz = {sign * b, (-sign) * n.z, 1.0f + ((sign * n.z) * n.z) * a};
+    return f;
+}
+
+// mapping.h:5-11 (local +y is the normal).
+SPT_HD V3 cosine_hemisphere(float xi_x, float xi_y) {
+    float sin_phi = sqrtf(1.0f - xi_x);
+    float theta = (kPi * 2.0f) * xi_y;
+    float s, c;
+    sincos_cephes(theta, s, c);
+    return {c * sin_phi, sqrtf(xi_x), s * sin_phi};
+}
+// mapping.h:15-27.
+SPT_HD void disk_from_square(float xi_x, float xi_y, float& ox, float& oy) {
+    float ax = xi_x * 2.0f - 1.0f, ay = xi_y * 2.0f - 1.0f;
+    float ax2 = ax * ax, ay2 = ay * ay;
+    bool cond = ax2 > ay2;
+    float r = cond ? ax : ay;
+    float phi = cond ? (kPi / 4.0f) * (ay / ax) : (kPi / 2.0f) - (kPi / 4.0f) * (ax / ay);
+    float s, c;
+    sincos_cephes(phi, s, c);
+    ox = r * c;
+    oy = r * s;
+}
+
+// ------------------------------------------------------------------ camera
+// ThinlensCamera (pinhole.h:7-72); the constants are computed once on the host.
+struct Camera {
+    V3 origin;
+    Frame frame;
+    float lens_radius, focal_dist, dist_lens_to_film, ratio, film_y;
+    float fw, fh;  // image resolution as float
+};
+
+// pinhole.h:27-32
+SPT_HD V3 camera_sample_pos(const Camera& c, float xi_x, float xi_y) {
+    float lx, ly;
+    disk_from_square(xi_x, xi_y, lx, ly);
+    lx = lx * c.lens_radius;
+    ly = ly * c.lens_radius;
+    V3 w = to_world(c.frame, v3(lx, 0.0f, ly));
+    return {w.x + c.origin.x, w.y + c.origin.y, w.z + c.origin.z};
+}
+// pinhole.h:34-56
+SPT_HD V3 camera_sample_dir(const Camera& c, uint32_t px, uint32_t py, V3 pos, float xi_x, float xi_y) {
+    V3 lens = to_local(c.frame, pos - c.origin);
+    float ndc_x = ((float)px + xi_x) / c.fw;
+    float ndc_y = ((float)py + xi_y) / c.fh;
+    float fx = (0.5f - ndc_x) * (c.ratio * c.film_y);
+    float fy = (0.5f - ndc_y) * c.film_y;
+    float fz = c.dist_lens_to_film;
+    V3 focal = {(c.focal_dist * fx) / fz, (c.focal_dist * fy) / fz, (c.focal_dist * fz) / fz};
+    return to_world(c.frame, normalize(focal - lens));
+}
+
+// --------------------------------------------------------------- triangles
+// Watertight ray/triangle test (Woop, Benthin, Wald 2013) standing in for
+// OptiX's built-in triangle intersector (optix_backend.h:314-324), with the
+// double-precision edge fallback.  Barycentrics follow OptiX / add_math.h:6:
+// p = (1-u-v) v0 + u v1 + v v2.
+struct WoopRay {
+    V3 o;
+    int kx, ky, kz;
+    float Sx, Sy, Sz;
+};
+SPT_HD WoopRay woop_setup(V3 o, V3 d) {
+    float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);
+    int kx = kz + 1; if (kx == 3) kx = 0;
+    int ky = kx + 1; if (ky == 3) ky = 0;
+    float dkz = comp(d, kz);
+    if (dkz < 0.0f) { int tmp = kx; kx = ky; ky = tmp; }
+    WoopRay r;
+    r.o = o; r.kx = kx; r.ky = ky; r.kz = kz;
+    r.Sx = comp(d, kx) / dkz;
+    r.Sy = comp(d, ky) / dkz;
+    r.Sz = 1.0f / dkz;
+    return r;
+}
+
+// Returns true with t/u/v when hit at t in [tmin, tmax] (NaN-safe).
+SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, float tmin, float tmax,
+                      float& t_out, float& u_out, float& v_out) {
+    V3 A = p0 - r.o, B = p1 - r.o, C = p2 - r.o;
+    float Akz = comp(A, r.kz), Bkz = comp(B, r.kz), Ckz = comp(C, r.kz);
+    float Ax = comp(A, r.kx) - r.Sx * Akz, Ay = comp(A, r.ky) - r.Sy * Akz;
+    float Bx = comp(B, r.kx) - r.Sx * Bkz, By = comp(B, r.ky) - r.Sy * Bkz;
+    float Cx = comp(C, r.kx) - r.Sx * Ckz, Cy = comp(C, r.ky) - r.Sy * Ckz;
+    float U = Cx * By - Cy * Bx;
+    float V = Ax * Cy - Ay * Cx;
+    float W = Bx * Ay - By * Ax;
+    if (U == 0.0f || V == 0.0f || W == 0.0f) {
+        U = (float)((double)Cx * (double)By - (double)Cy * (double)Bx);
+        V = (float)((double)Ax * (double)Cy - (double)Ay * (double)Cx);
+        W = (float)((double)Bx * (double)Ay - (double)By * (double)Ax);
+    }
+    if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
+    float det = (U + V) + W;
+    if (det == 0.0f) return false;
+    float Az = r.Sz * Akz, Bz = r.Sz * Bkz, Cz = r.Sz * Ckz;
+    float T = (U * Az + V * Bz) + W * Cz;
+    float t = T / det;
+    if (!(t >= tmin && t <= tmax)) return false;
+    t_out = t;
+    u_out = V / det;
+    v_out = W / det;
+    return true;
+}
+
+// ------------------------------------------------------------ roulette
+// Russian-roulette side stream (a build addition: the reference has none,
+// SURVEY F7/A14).  Counter-based so the 4+2D PCG32 draw layout is untouched.
+SPT_HD float rr_uniform(uint32_t pixel, uint32_t sample, uint32_t depth) {
+    uint32_t h = pixel * 0x9E3779B1u ^ (sample + 0x7F4A7C15u) * 0x85EBCA77u ^ (depth + 1u) * 0xC2B2AE3Du;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return (float)(h >> 8) * (1.0f / 16777216.0f);
+}
+
+}  // namespace spt

@@ -1,0 +1,11 @@
+"""sptamd — host side of the MI355X-native wavefront path tracer.
+
+Importing this package loads libspt.so (HIP kernels for gfx950 behind the C
+ABI of include/spt.h) and fails loudly when it has not been built.
+"""
+from . import _lib
+from ._lib import SptError, check, default_params, lib, tile_rows
+from .backend import HipBackend, Ray3, Scene, TriangleHitInfo, make_params, reference_camera, write_pfm
+
+__all__ = ["_lib", "SptError", "check", "default_params", "lib", "tile_rows", "HipBackend", "Ray3", "Scene",
+           "TriangleHitInfo", "make_params", "reference_camera", "write_pfm"]

@@ -1,0 +1,150 @@
+"""ctypes binding of include/spt.h (libspt.so, built in-tree by the Makefile).
+
+The library is the only compute path: if it is missing, import fails loudly
+(there is no CPU fallback in the product).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_uint8, c_uint32, c_uint64, c_void_p
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "build", "libspt.so")
+
+SPT_OK = 0
+SPT_RNG_Y_FIRST = 0
+SPT_RNG_X_FIRST = 1
+SPT_FLAG_TIMING = 1
+PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
+
+# Every function include/spt.h declares (the CPU test checks they are exported).
+EXPORTED = [
+    "spt_init", "spt_scene_create", "spt_scene_set_albedo", "spt_scene_get_stats",
+    "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
+    "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
+    "spt_obj_load", "spt_mesh_free", "spt_pfm_write",
+]
+
+
+class SptError(RuntimeError):
+    """Raised for a non-zero spt_status (the reference throws std::runtime_error
+    from OPTIX_CHECK / CUDA_CHECK, optix_backend.h:25-66)."""
+
+    def __init__(self, what: str, code: int, msg: str):
+        super().__init__(f"{what} failed ({code}): {msg}")
+        self.code = code
+
+
+class Rays(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("ox", "oy", "oz", "dx", "dy", "dz", "tmin", "tmax")]
+
+
+class Hits(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("tri_id", "t", "u", "v")]
+
+
+class HitInfo(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("px", "py", "pz", "gnx", "gny", "gnz", "snx", "sny", "snz",
+                                        "tcu", "tcv", "mat_id")]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("look_from", c_float * 3), ("look_at", c_float * 3), ("up", c_float * 3),
+                ("lens_radius", c_float), ("focal_dist", c_float), ("fov_y", c_float),
+                ("film_size_y", c_float)]
+
+
+class RenderParams(ctypes.Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_depth", c_uint32),
+                ("camera", Camera),
+                ("tile_index", c_uint32), ("tile_count", c_uint32), ("rows_per_group", c_uint32),
+                ("paths_per_pixel", c_uint32), ("rr_start_depth", c_uint32), ("rng_order", c_uint32),
+                ("rng_initstate", c_uint64), ("env", c_float * 3), ("flags", c_uint32)]
+
+
+class RenderStats(ctypes.Structure):
+    _fields_ = [("paths", c_uint64), ("ray_casts", c_uint64), ("continuations", c_uint64),
+                ("regenerations", c_uint64), ("iterations", c_uint64),
+                ("paths_in_flight", c_uint32), ("tile_rows", c_uint32),
+                ("isect_ms", c_double), ("shade_ms", c_double), ("camera_ms", c_double),
+                ("resolve_ms", c_double), ("total_ms", c_double)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class SceneStats(ctypes.Structure):
+    _fields_ = [("ntri", c_uint64), ("nodes", c_uint64), ("leaves", c_uint64),
+                ("max_depth", c_uint32), ("max_leaf", c_uint32), ("device_bytes", c_uint64),
+                ("build_ms", c_double), ("sah_cost", c_double)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class Mesh(ctypes.Structure):
+    _fields_ = [("pos_tri", POINTER(c_int32)), ("pos", POINTER(c_float)), ("nvert", c_uint64), ("ntri", c_uint64),
+                ("nrm_tri", POINTER(c_int32)), ("nrm", POINTER(c_float)), ("nnrm", c_uint64),
+                ("tc_tri", POINTER(c_int32)), ("tc", POINTER(c_float)), ("ntc", c_uint64),
+                ("mat_id", POINTER(c_int32)), ("kd", POINTER(c_float)), ("nmat", c_uint32)]
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libspt.so not built at {LIB_PATH}: run `make -C smallpt-enoki-optix_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    i32, u32, u64, vp = c_int32, c_uint32, c_uint64, c_void_p
+    sig = {
+        "spt_init": (i32, [i32]),
+        "spt_scene_create": (i32, [vp, vp, u64, u64, vp, vp, u64, vp, vp, u64, vp, POINTER(vp)]),
+        "spt_scene_set_albedo": (i32, [vp, vp, u32]),
+        "spt_scene_get_stats": (i32, [vp, POINTER(SceneStats)]),
+        "spt_scene_destroy": (i32, [vp]),
+        "spt_intersect": (i32, [vp, POINTER(Rays), vp, u32, POINTER(Hits), u32, i32, vp]),
+        "spt_hit_info_compute": (i32, [vp, POINTER(Rays), POINTER(Hits), vp, u32, u32, POINTER(HitInfo), vp]),
+        "spt_render": (i32, [vp, POINTER(RenderParams), vp, POINTER(RenderStats), vp]),
+        "spt_tile_rows": (u32, [u32, u32, u32, u32, vp, u32]),
+        "spt_default_params": (None, [POINTER(RenderParams)]),
+        "spt_last_error": (c_char_p, []),
+        "spt_version": (c_char_p, []),
+        "spt_obj_load": (i32, [c_char_p, POINTER(Mesh)]),
+        "spt_mesh_free": (None, [POINTER(Mesh)]),
+        "spt_pfm_write": (i32, [c_char_p, vp, vp, vp, u32, u32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int, what: str) -> None:
+    if status != SPT_OK:
+        raise SptError(what, status, lib.spt_last_error().decode(errors="replace"))
+
+
+def default_params() -> RenderParams:
+    p = RenderParams()
+    lib.spt_default_params(ctypes.byref(p))
+    return p
+
+
+def tile_rows(height: int, tile_index: int, tile_count: int, rows_per_group: int):
+    import numpy as np
+    n = lib.spt_tile_rows(height, tile_index, tile_count, rows_per_group, None, 0)
+    rows = np.zeros(max(n, 1), dtype=np.uint32)
+    lib.spt_tile_rows(height, tile_index, tile_count, rows_per_group, rows.ctypes.data, n)
+    return rows[:n].astype(np.int64)
+
+
+__all__ = [
+    "lib", "check", "SptError", "Rays", "Hits", "HitInfo", "Camera", "RenderParams", "RenderStats",
+    "SceneStats", "Mesh", "default_params", "tile_rows", "EXPORTED", "LIB_PATH", "REPO_ROOT",
+    "PCG32_DEFAULT_STATE", "SPT_RNG_Y_FIRST", "SPT_RNG_X_FIRST", "SPT_FLAG_TIMING", "c_uint8",
+]

@@ -1,0 +1,264 @@
+"""Python host mirror of the reference's hot-path interface, over libspt.so.
+
+    HipBackend   <-> OptixBackend        (src/accel/optix_backend.h:164-504)
+    Ray3         <-> Ray<Real3C>         (src/ray.h:5-36)
+    TriangleHitInfo <-> TriangleHitInfo  (src/accel/optix_backend.h:99-134)
+    Scene        <-> Scene               (src/main.cpp:286-352)
+    Scene.render <-> main() render loop  (src/main.cpp:354-429)
+
+Device memory and streams come from torch (HIP tensors); every computation
+runs in the HIP kernels of libspt.so.  Errors raise SptError, as the
+reference's OPTIX_CHECK / CUDA_CHECK raise std::runtime_error.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import Hits, HitInfo, Rays, RenderParams, RenderStats, SceneStats, check, lib
+
+RAY_TMIN = 0.001  # ray.h:16
+RAY_TMAX = 1e20
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]) -> Optional[int]:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream or None
+
+
+def _dev_f32(x, device) -> torch.Tensor:
+    t = torch.as_tensor(x, dtype=torch.float32)
+    return t.to(device).contiguous()
+
+
+def _host_ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+@dataclass
+class Ray3:
+    """SoA rays (ray.h:28-31).  origin/dir: (3, N) float32 device tensors."""
+
+    origin: torch.Tensor
+    dir: torch.Tensor
+    tmin: torch.Tensor
+    tmax: torch.Tensor
+
+    @staticmethod
+    def make(origin, direction, tmin: float = RAY_TMIN, tmax: float = RAY_TMAX, device="cuda") -> "Ray3":
+        o = _dev_f32(origin, device)
+        d = _dev_f32(direction, device)
+        n = o.shape[1]
+        return Ray3(o, d, torch.full((n,), tmin, dtype=torch.float32, device=o.device),
+                    torch.full((n,), tmax, dtype=torch.float32, device=o.device))
+
+    def __len__(self) -> int:
+        return int(self.origin.shape[1])
+
+    def c_struct(self) -> Rays:
+        return Rays(self.origin[0].data_ptr(), self.origin[1].data_ptr(), self.origin[2].data_ptr(),
+                    self.dir[0].data_ptr(), self.dir[1].data_ptr(), self.dir[2].data_ptr(),
+                    self.tmin.data_ptr(), self.tmax.data_ptr())
+
+
+@dataclass
+class TriangleHitInfo:
+    """optix_backend.h:99-134; device tensors, planar (3, N) vectors."""
+
+    tri_id: torch.Tensor
+    t: torch.Tensor
+    barycentric: torch.Tensor
+    position: torch.Tensor
+    geometry_normal: torch.Tensor
+    shading_normal: torch.Tensor
+    texcoord: torch.Tensor
+    material_id: torch.Tensor
+
+
+class HipBackend:
+    """OptixBackend replacement: init / set_triangles_soup / intersect."""
+
+    def __init__(self):
+        self._scene = ctypes.c_void_p()
+        self.device = None
+        self.stats: dict = {}
+
+    def __del__(self):
+        if getattr(self, "_scene", None) and self._scene.value:
+            lib.spt_scene_destroy(self._scene)
+            self._scene = ctypes.c_void_p()
+
+    # optix_backend.h:178-186
+    def init(self, device: int = 0) -> None:
+        check(lib.spt_init(device), "spt_init")
+        self.device = torch.device("cuda", device)
+
+    # optix_backend.h:283-364 (arrays are host arrays here; the BVH is built on the host)
+    def set_triangles_soup(self, position_triplets, positions, shading_normal_triplets=None, shading_normals=None,
+                           texcoord_triplets=None, texcoords=None, material_ids=None) -> None:
+        if self.device is None:
+            self.init(0)
+        pt = np.ascontiguousarray(np.asarray(position_triplets, dtype=np.int32).reshape(-1))
+        pos = np.ascontiguousarray(np.asarray(positions, dtype=np.float32).reshape(-1))
+        nt = None if shading_normal_triplets is None else np.ascontiguousarray(
+            np.asarray(shading_normal_triplets, dtype=np.int32).reshape(-1))
+        nrm = None if shading_normals is None else np.ascontiguousarray(
+            np.asarray(shading_normals, dtype=np.float32).reshape(-1))
+        tt = None if texcoord_triplets is None else np.ascontiguousarray(
+            np.asarray(texcoord_triplets, dtype=np.int32).reshape(-1))
+        tc = None if texcoords is None else np.ascontiguousarray(np.asarray(texcoords, dtype=np.float32).reshape(-1))
+        mat = None if material_ids is None else np.ascontiguousarray(np.asarray(material_ids, dtype=np.int32).reshape(-1))
+        ntri = pt.size // 3
+        if self._scene.value:
+            lib.spt_scene_destroy(self._scene)
+            self._scene = ctypes.c_void_p()
+        check(lib.spt_scene_create(
+            _host_ptr(pt), _host_ptr(pos), pos.size // 3, ntri,
+            _host_ptr(nt), _host_ptr(nrm), 0 if nrm is None else nrm.size // 3,
+            _host_ptr(tt), _host_ptr(tc), 0 if tc is None else tc.size // 2,
+            _host_ptr(mat), ctypes.byref(self._scene)), "spt_scene_create")
+        st = SceneStats()
+        check(lib.spt_scene_get_stats(self._scene, ctypes.byref(st)), "spt_scene_get_stats")
+        self.stats = st.as_dict()
+
+    def set_albedo(self, albedo_rgb) -> None:
+        a = np.ascontiguousarray(np.asarray(albedo_rgb, dtype=np.float32).reshape(-1, 3))
+        check(lib.spt_scene_set_albedo(self._scene, a.ctypes.data, a.shape[0]), "spt_scene_set_albedo")
+
+    @property
+    def handle(self):
+        return self._scene
+
+    def intersect_raw(self, rays: Ray3, mask=None, do_closest: bool = True, stream=None,
+                      out: Optional[Sequence[torch.Tensor]] = None):
+        """__raygen__rg semantics (wavefront_isect.cu:80-112).  Returns
+        (tri_id, t, u, v); masked lanes keep `out`'s values (default -1/0)."""
+        n = len(rays)
+        dev = rays.origin.device
+        if out is None:
+            tri_id = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            t = torch.zeros(n, dtype=torch.float32, device=dev)
+            u = torch.zeros(n, dtype=torch.float32, device=dev)
+            v = torch.zeros(n, dtype=torch.float32, device=dev)
+        else:
+            tri_id, t, u, v = out
+        mask_ptr, mask_size = None, 0
+        if mask is not None:
+            m = torch.as_tensor(mask, dtype=torch.uint8).to(dev).contiguous().reshape(-1)
+            mask_ptr, mask_size = m.data_ptr(), m.numel()
+        hits = Hits(tri_id.data_ptr(), t.data_ptr(), u.data_ptr(), v.data_ptr())
+        rs = rays.c_struct()
+        check(lib.spt_intersect(self._scene, ctypes.byref(rs), mask_ptr, mask_size, ctypes.byref(hits), n,
+                                1 if do_closest else 0, _stream_handle(stream)), "spt_intersect")
+        self._keep = mask  # keep the mask alive until the stream is synchronised by the caller
+        return tri_id, t, u, v
+
+    # optix_backend.h:422-487
+    def intersect(self, rays: Ray3, mask=None, stream=None):
+        tri_id, t, u, v = self.intersect_raw(rays, mask, True, stream)
+        n = len(rays)
+        dev = rays.origin.device
+        z3 = lambda: torch.zeros((3, n), dtype=torch.float32, device=dev)  # noqa: E731
+        pos, gn, sn, tc = z3(), z3(), z3(), torch.zeros((2, n), dtype=torch.float32, device=dev)
+        mat = torch.zeros(n, dtype=torch.int32, device=dev)
+        info = HitInfo(pos[0].data_ptr(), pos[1].data_ptr(), pos[2].data_ptr(),
+                       gn[0].data_ptr(), gn[1].data_ptr(), gn[2].data_ptr(),
+                       sn[0].data_ptr(), sn[1].data_ptr(), sn[2].data_ptr(),
+                       tc[0].data_ptr(), tc[1].data_ptr(), mat.data_ptr())
+        mask_ptr, mask_size = None, 0
+        if mask is not None:
+            m = torch.as_tensor(mask, dtype=torch.uint8).to(dev).contiguous().reshape(-1)
+            mask_ptr, mask_size = m.data_ptr(), m.numel()
+        rs = rays.c_struct()
+        hits = Hits(tri_id.data_ptr(), t.data_ptr(), u.data_ptr(), v.data_ptr())
+        check(lib.spt_hit_info_compute(self._scene, ctypes.byref(rs), ctypes.byref(hits), mask_ptr, mask_size, n,
+                                       ctypes.byref(info), _stream_handle(stream)), "spt_hit_info_compute")
+        active = tri_id != -1                                              # optix_backend.h:463
+        if mask is not None:
+            mt = torch.as_tensor(mask, dtype=torch.bool).to(dev).reshape(-1)
+            active = active & (mt if mt.numel() == n else mt.expand(n))
+        hit = TriangleHitInfo(tri_id, t, torch.stack([u, v]), pos, gn, sn, tc, mat)
+        return hit, active
+
+
+def reference_camera() -> dict:
+    """ThinlensCamera at main.cpp:383."""
+    return dict(look_from=(0.0, 3.03, 5.0), look_at=(0.0, 0.03, 0.0), up=(0.0, 1.0, 0.0), lens_radius=0.0,
+                focal_dist=1.0, fov_y=float(np.float32(np.float32(40.0) / np.float32(180.0)) * np.float32(math.pi)),
+                film_size_y=0.035)
+
+
+def make_params(width: int, height: int, spp: int, max_depth: int, camera: Optional[dict] = None,
+                tile_index: int = 0, tile_count: int = 1, rows_per_group: int = 1, paths_per_pixel: int = 0,
+                rr_start_depth: int = 1, rng_order: int = 0, env=(1.0, 1.0, 1.0), timing: bool = False,
+                rng_initstate: int = _lib.PCG32_DEFAULT_STATE) -> RenderParams:
+    p = _lib.default_params()
+    p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
+    cam = reference_camera() if camera is None else camera
+    for k in ("look_from", "look_at", "up"):
+        getattr(p.camera, k)[:] = [float(x) for x in cam[k]]
+    p.camera.lens_radius = cam["lens_radius"]
+    p.camera.focal_dist = cam["focal_dist"]
+    p.camera.fov_y = cam["fov_y"]
+    p.camera.film_size_y = cam["film_size_y"]
+    p.tile_index, p.tile_count, p.rows_per_group = tile_index, tile_count, rows_per_group
+    p.paths_per_pixel = paths_per_pixel
+    p.rr_start_depth = rr_start_depth
+    p.rng_order = rng_order
+    p.rng_initstate = rng_initstate
+    p.env[:] = [float(e) for e in env]
+    p.flags = _lib.SPT_FLAG_TIMING if timing else 0
+    return p
+
+
+class Scene:
+    """main.cpp:286-352: add_triangle_mesh / commit / intersect, plus render()."""
+
+    def __init__(self):
+        self.backend = HipBackend()
+        self.mesh = None
+
+    def add_triangle_mesh(self, obj_path: str) -> None:   # main.cpp:288-310
+        from .scenes import load_obj
+        self.mesh = load_obj(obj_path)
+
+    def add_arrays(self, mesh: dict) -> None:
+        self.mesh = mesh
+
+    def commit(self, device: int = 0) -> None:             # main.cpp:312-318
+        m = self.mesh
+        self.backend.init(device)
+        self.backend.set_triangles_soup(m["pos_tri"], m["pos"], m.get("nrm_tri"), m.get("nrm"), m.get("tc_tri"),
+                                        m.get("tc"), m.get("mat_id"))
+        if m.get("albedo") is not None:
+            self.backend.set_albedo(m["albedo"])
+
+    def intersect(self, ray: Ray3, active=None):           # main.cpp:320-340
+        return self.backend.intersect(ray, active)
+
+    def render(self, params: RenderParams, film: Optional[torch.Tensor] = None, stream=None):
+        """One wavefront render of params' tile.  Returns (film (3, rows, W)
+        float32 on the device, stats dict)."""
+        rows = lib.spt_tile_rows(params.height, params.tile_index, params.tile_count, params.rows_per_group,
+                                 None, 0)
+        if film is None:
+            film = torch.empty((3, rows, params.width), dtype=torch.float32, device=self.backend.device)
+        assert film.is_contiguous() and film.numel() >= 3 * rows * params.width
+        st = RenderStats()
+        check(lib.spt_render(self.backend.handle, ctypes.byref(params), film.data_ptr(), ctypes.byref(st),
+                             _stream_handle(stream)), "spt_render")
+        return film, st.as_dict()
+
+
+def write_pfm(path: str, film: np.ndarray) -> None:
+    """Fimage::save_pfm via the C ABI; film: (3, H, W) float32 host array."""
+    f = np.ascontiguousarray(film, dtype=np.float32)
+    _, h, w = f.shape
+    check(lib.spt_pfm_write(path.encode(), f[0].ctypes.data, f[1].ctypes.data, f[2].ctypes.data, w, h),
+          "spt_pfm_write")

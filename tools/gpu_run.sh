@@ -1,0 +1,36 @@
+#!/bin/bash
+# GPU-box driver: each step under its own timeout; stop at the first step that
+# faults / aborts / times out (exit 124, 134, 137, 139 or > 128).  Test
+# failures (pytest exit 1) do not stop the later steps.
+# usage: tools/gpu_run.sh step1 step2 ...   (steps: smoke tests bench prof pmc)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" | tee -a gpurun_out/steps.log
+  local t0=$(date +%s)
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(( $(date +%s) - t0 ))s" | tee -a gpurun_out/steps.log
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "STOP: $name ended with $rc" | tee -a gpurun_out/steps.log
+    exit $rc
+  fi
+  return 0
+}
+for s in "$@"; do
+  case "$s" in
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    tests) run tests 900 python -m pytest tests -m gpu -q -x ;;
+    testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
+    bench) run bench 600 python bench.py ;;
+    benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
