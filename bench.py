@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--scene", default="mitsuba_synth")
     ap.add_argument("--rows-per-group", type=int, default=8)
-    ap.add_argument("--ppp", type=int, default=0, help="paths per pixel in flight (0 = auto)")
+    ap.add_argument("--wavefront", type=int, default=0, help="paths in flight per launch (0 = auto)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -106,7 +106,7 @@ def main():
     W, H = args.width, args.height
     R = args.rows_per_group
     params = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
-                                paths_per_pixel=args.ppp, timing=True)
+                                wavefront_paths=args.wavefront, timing=True)
     rows_all = [sptamd.tile_rows(H, r, world, R) for r in range(world)]
     max_rows = max(len(r) for r in rows_all)
     dev = torch.device("cuda", local)

@@ -87,7 +87,7 @@ typedef struct spt_render_params {
     /* Interleaved row-group tiling: global row r belongs to tile
      * (r / rows_per_group) % tile_count.  tile_count = 1 renders the image. */
     uint32_t tile_index, tile_count, rows_per_group;
-    uint32_t paths_per_pixel;   /* samples of one pixel in flight (0 = auto) */
+    uint32_t wavefront_paths;   /* paths in flight per launch (0 = auto, ~2M) */
     uint32_t rr_start_depth;    /* Russian roulette from this cast on (>= max_depth: off) */
     uint32_t rng_order;         /* SPT_RNG_* */
     uint64_t rng_initstate;     /* PCG32_DEFAULT_STATE 0x853c49e6748fea9b (main.cpp:376) */
@@ -99,11 +99,11 @@ typedef struct spt_render_stats {
     uint64_t paths;             /* pixels x spp rendered by this call */
     uint64_t ray_casts;         /* closest/any-hit queries traced */
     uint64_t continuations;     /* paths that bounced into a next cast */
-    uint64_t regenerations;     /* camera rays started in-loop (path regeneration) */
+    uint64_t regenerations;     /* camera rays started by refills after the first launch */
     uint64_t iterations;        /* isect+shade launch pairs */
-    uint32_t paths_in_flight;   /* wavefront capacity (tile pixels x paths_per_pixel) */
+    uint32_t paths_in_flight;   /* wavefront capacity (queue slots) */
     uint32_t tile_rows;
-    double isect_ms, shade_ms, camera_ms, resolve_ms; /* SPT_FLAG_TIMING only */
+    double isect_ms, shade_ms, camera_ms, resolve_ms; /* SPT_FLAG_TIMING only (camera = refills) */
     double total_ms;            /* host wall time of the call (includes final sync) */
 } spt_render_stats;
 

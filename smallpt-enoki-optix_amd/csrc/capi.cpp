@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -65,21 +66,32 @@ PathQueue carve_queue(char* base, size_t cap) {
     return q;
 }
 
+// Device counters of one render (zeroed per call; see spt_render).
+struct Counters {
+    uint32_t qn[2];      // queue counts (isect/shade input)
+    uint32_t surv[2];    // survivors appended by shade
+    uint64_t cursor[2];  // next work item (double-buffered across refills)
+    unsigned long long stats[3];  // casts, continuations, camera rays started
+};
+
 struct Workspace {
-    size_t cap = 0, film_cap = 0;
+    size_t cap = 0, film_cap = 0, jump_cap = 0;
     char* qa = nullptr;
     char* qb = nullptr;
     char* hits = nullptr;
     float* film = nullptr;
-    uint32_t* counts = nullptr;             // [0], [1] queue counts
-    unsigned long long* stats = nullptr;    // casts, continuations, regenerations
+    PcgJump* jumps = nullptr;
+    uint32_t jump_key_spp = 0, jump_key_depth = 0;
+    Counters* counters = nullptr;
     uint32_t* host_counts = nullptr;        // pinned, 2 slots
+    uint64_t* host_cursor = nullptr;        // pinned, 2 slots
     std::vector<hipEvent_t> events;
     hipEvent_t count_ev[2] = {nullptr, nullptr};
 
     void release() {
-        hfree(qa); hfree(qb); hfree(hits); hfree(film); hfree(counts);
+        hfree(qa); hfree(qb); hfree(hits); hfree(film); hfree(counters); hfree(jumps);
         if (host_counts) (void)hipHostFree(host_counts);
+        if (host_cursor) (void)hipHostFree(host_cursor);
         for (auto e : events) (void)hipEventDestroy(e);
         for (auto& e : count_ev) if (e) (void)hipEventDestroy(e);
         *this = Workspace();
@@ -155,7 +167,7 @@ Camera make_camera(const spt_render_params& p) {
     return cam;
 }
 
-spt_status ensure_workspace(Workspace& ws, size_t cap, size_t film_floats) {
+spt_status ensure_workspace(Workspace& ws, size_t cap, size_t film_floats, size_t njumps) {
     if (cap > ws.cap) {
         hfree(ws.qa); hfree(ws.qb); hfree(ws.hits);
         ws.cap = 0;
@@ -170,11 +182,16 @@ spt_status ensure_workspace(Workspace& ws, size_t cap, size_t film_floats) {
         HIP_TRY(hipMalloc((void**)&ws.film, sizeof(float) * film_floats));
         ws.film_cap = film_floats;
     }
-    if (!ws.counts) {
-        HIP_TRY(hipMalloc((void**)&ws.counts, 64));
-        ws.stats = (unsigned long long*)((char*)ws.counts + 16);
+    if (njumps > ws.jump_cap) {
+        hfree(ws.jumps);
+        ws.jump_cap = 0;
+        ws.jump_key_spp = 0;
+        HIP_TRY(hipMalloc((void**)&ws.jumps, sizeof(PcgJump) * njumps));
+        ws.jump_cap = njumps;
     }
+    if (!ws.counters) HIP_TRY(hipMalloc((void**)&ws.counters, sizeof(Counters)));
     if (!ws.host_counts) HIP_TRY(hipHostMalloc((void**)&ws.host_counts, 16, hipHostMallocDefault));
+    if (!ws.host_cursor) HIP_TRY(hipHostMalloc((void**)&ws.host_cursor, 16, hipHostMallocDefault));
     for (auto& e : ws.count_ev)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return SPT_OK;
@@ -217,7 +234,7 @@ void spt_default_params(spt_render_params* p) {
     p->camera.fov_y = 40.0f / 180.0f * (float)M_PI;
     p->camera.film_size_y = 0.035f;                                    // pinhole.h:11
     p->tile_index = 0; p->tile_count = 1; p->rows_per_group = 1;
-    p->paths_per_pixel = 0;
+    p->wavefront_paths = 0;
     p->rr_start_depth = 1;
     p->rng_order = SPT_RNG_Y_FIRST;
     p->rng_initstate = kPcgDefaultState;
@@ -408,7 +425,7 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
 spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev, spt_render_stats* stats_out,
                       void* stream_) {
     const double wall0 = now_ms();
-    if (!sc || !pp || !film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL argument");
+    if (!sc || !pp) return fail(SPT_ERR_INVALID, "spt_render: NULL argument");
     const spt_render_params& p = *pp;
     if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
         return fail(SPT_ERR_INVALID, "spt_render: width/height/spp/max_depth must be > 0");
@@ -425,54 +442,64 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     spt_render_stats rs{};
     rs.tile_rows = rows;
     rs.paths = P * p.spp;
-    if (P == 0) {
+    if (P == 0) {  // an empty tile: nothing to render, film untouched
         if (stats_out) *stats_out = rs;
         return SPT_OK;
     }
-    // Paths in flight: enough lanes to fill 256 CUs (~1M) but at most spp per pixel.
-    uint64_t k = p.paths_per_pixel;
-    if (k == 0) {
-        const uint64_t target = 1ull << 20;
-        k = (target + P - 1) / P;
-    }
-    k = std::max<uint64_t>(1, std::min<uint64_t>(k, p.spp));
-    const uint64_t C = P * k;
-    if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: %llu paths in flight exceeds 2^31", (unsigned long long)C);
+    if (!film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
+
+    // Wavefront capacity: enough lanes to keep 256 CUs busy through a launch.
+    uint64_t C = p.wavefront_paths ? p.wavefront_paths : (1ull << 21);
+    C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
+    if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
+                                       (unsigned long long)C);
+    // Per-sample contribution film [chunk][3][P], at most ~4 GiB per chunk.
+    const uint64_t budget = 4ull << 30;
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(p.spp, budget / (12 * P)));
     rs.paths_in_flight = (uint32_t)C;
-    spt_status st = ensure_workspace(sc->ws, C, (size_t)k * 3 * P);
+    spt_status st = ensure_workspace(sc->ws, C, (size_t)chunk * 3 * P + 3 * P, p.spp);
     if (st) return st;
     Workspace& ws = sc->ws;
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
 
+    // PCG32 jump to each sample's first draw: s * (4 + 2D) (main.cpp:395,396,413).
+    const uint64_t per_sample = 4ull + 2ull * p.max_depth;
+    if (ws.jump_key_spp != p.spp || ws.jump_key_depth != p.max_depth) {
+        std::vector<PcgJump> jt(p.spp);
+        for (uint32_t s = 0; s < p.spp; s++) jt[s] = pcg_jump_coeffs((uint64_t)s * per_sample);
+        HIP_TRY(hipMemcpy(ws.jumps, jt.data(), sizeof(PcgJump) * p.spp, hipMemcpyHostToDevice));
+        ws.jump_key_spp = p.spp;
+        ws.jump_key_depth = p.max_depth;
+    }
+
     const Camera cam = make_camera(p);
-    PathQueue qa = carve_queue(ws.qa, ws.cap), qb = carve_queue(ws.qb, ws.cap);
+    PathQueue q[2] = {carve_queue(ws.qa, ws.cap), carve_queue(ws.qb, ws.cap)};
     int32_t* hit_slot = (int32_t*)ws.hits;
     float* hit_t = (float*)(hit_slot + ws.cap);
     float* hit_u = hit_t + ws.cap;
     float* hit_v = hit_u + ws.cap;
+    float* sfilm = ws.film;
+    float* acc = ws.film + (size_t)chunk * 3 * P;
+    Counters* cnt = ws.counters;
 
-    HIP_TRY(hipMemsetAsync(ws.film, 0, sizeof(float) * k * 3 * P, stream));
-    HIP_TRY(hipMemsetAsync(ws.counts, 0, 64, stream));
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)ws.counts, (int)C, 1, stream));
-
+    HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(Counters), stream));
+    std::vector<std::pair<size_t, int>> timed;  // (start event index, 0 refill 1 isect 2 shade 3 resolve)
     size_t ev = 0;
-    hipEvent_t e0, e1;
-    if (timing) {
-        if ((st = get_event(ws, ev++, &e0))) return st;
-        HIP_TRY(hipEventRecord(e0, stream));
-    }
-    CameraInitArgs ca;
-    ca.q = qa; ca.cam = cam; ca.P = (uint32_t)P; ca.W = p.width; ca.k_eff = (uint32_t)k;
-    ca.max_depth = p.max_depth; ca.rng_order = p.rng_order;
-    ca.tile_index = p.tile_index; ca.tile_count = p.tile_count; ca.rows_per_group = p.rows_per_group;
-    ca.initstate = p.rng_initstate;
-    HIP_TRY(launch_camera_init(ca, (uint32_t)C, stream));
-    if (timing) {
-        if ((st = get_event(ws, ev++, &e1))) return st;
-        HIP_TRY(hipEventRecord(e1, stream));
-    }
-    std::vector<std::pair<size_t, int>> timed;  // (event index of start, kind 0 cam 1 isect 2 shade 3 resolve)
-    if (timing) timed.push_back({0, 0});
+    auto mark = [&](int kind, auto&& launch) -> spt_status {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        spt_status s2;
+        if (timing) {
+            if ((s2 = get_event(ws, ev, &e0)) || (s2 = get_event(ws, ev + 1, &e1))) return s2;
+            HIP_TRY(hipEventRecord(e0, stream));
+        }
+        HIP_TRY(launch());
+        if (timing) {
+            HIP_TRY(hipEventRecord(e1, stream));
+            timed.push_back({ev, kind});
+            ev += 2;
+        }
+        return SPT_OK;
+    };
 
     IsectQueueArgs ia;
     ia.sc = sc->dev();
@@ -481,92 +508,90 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     ShadeArgs sa;
     sa.sc = sc->dev();
     sa.hit_slot = hit_slot; sa.hit_t = hit_t; sa.hit_u = hit_u; sa.hit_v = hit_v;
-    sa.film = ws.film;
-    sa.stats = ws.stats;
-    sa.cam = cam;
-    sa.P = (uint32_t)P; sa.W = p.width; sa.k = (uint32_t)k; sa.spp = p.spp; sa.max_depth = p.max_depth;
+    sa.sfilm = sfilm;
+    sa.stats = cnt->stats;
+    sa.P = (uint32_t)P; sa.W = p.width; sa.max_depth = p.max_depth;
     sa.rr_start = p.rr_start_depth; sa.rng_order = p.rng_order;
     sa.tile_index = p.tile_index; sa.tile_count = p.tile_count; sa.rows_per_group = p.rows_per_group;
     sa.env_r = p.env[0]; sa.env_g = p.env[1]; sa.env_b = p.env[2];
-    const uint64_t per_sample = 4ull + 2ull * p.max_depth;
-    for (uint32_t pairs = 0; pairs <= p.max_depth; pairs++)
-        sa.jumps[pairs] = pcg_jump_coeffs(2ull * (p.max_depth - pairs) + (k - 1) * per_sample);
+    RefillArgs ra;
+    ra.cam = cam;
+    ra.sample_jump = ws.jumps;
+    ra.stats = cnt->stats;
+    ra.capacity = (uint32_t)C; ra.P = (uint32_t)P; ra.W = p.width; ra.rng_order = p.rng_order;
+    ra.tile_index = p.tile_index; ra.tile_count = p.tile_count; ra.rows_per_group = p.rows_per_group;
+    ra.initstate = p.rng_initstate;
 
-    // Iterate isect -> shade until the queue drains.  The live count never
-    // grows, so a stale (larger) host copy is a safe grid size; it is read
-    // back once per batch, pipelined one batch behind the launches.
-    const uint64_t max_iters = ((uint64_t)p.spp + k - 1) / k * p.max_depth + 4ull * p.max_depth + 64;
-    uint32_t known = (uint32_t)C;
     uint64_t iters = 0;
-    int cur = 0;
-    int pending = -1;
-    uint32_t batch = 4, nbatch = 0;
-    while (true) {
-        for (uint32_t b = 0; b < batch; b++) {
-            PathQueue& qin = cur == 0 ? qa : qb;
-            PathQueue& qout = cur == 0 ? qb : qa;
-            ia.q = qin;
-            ia.count = ws.counts + cur;
-            if (timing) {
-                if ((st = get_event(ws, ev, &e0))) return st;
-                HIP_TRY(hipEventRecord(e0, stream));
-                timed.push_back({ev, 1});
-                ev += 2;
-            }
-            HIP_TRY(launch_isect_queue(ia, known, stream));
-            if (timing) {
-                if ((st = get_event(ws, ev - 1, &e1))) return st;
-                HIP_TRY(hipEventRecord(e1, stream));
-            }
-            HIP_TRY(hipMemsetAsync(ws.counts + (1 - cur), 0, sizeof(uint32_t), stream));
-            sa.in = qin; sa.out = qout;
-            sa.count_in = ws.counts + cur;
-            sa.count_out = ws.counts + (1 - cur);
-            if (timing) {
-                if ((st = get_event(ws, ev, &e0))) return st;
-                HIP_TRY(hipEventRecord(e0, stream));
-                timed.push_back({ev, 2});
-                ev += 2;
-            }
-            HIP_TRY(launch_shade(sa, known, stream));
-            if (timing) {
-                if ((st = get_event(ws, ev - 1, &e1))) return st;
-                HIP_TRY(hipEventRecord(e1, stream));
-            }
-            cur = 1 - cur;
-            iters++;
-        }
-        const int slot = (int)(nbatch++ & 1u);
-        HIP_TRY(hipMemcpyAsync(ws.host_counts + slot, ws.counts + cur, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        HIP_TRY(hipEventRecord(ws.count_ev[slot], stream));
-        if (pending >= 0) {
-            HIP_TRY(hipEventSynchronize(ws.count_ev[pending]));
-            known = ws.host_counts[pending];
-            if (known == 0) break;
-        }
-        pending = slot;
-        if (iters > max_iters)
-            return fail(SPT_ERR_HIP, "spt_render: queue did not drain after %llu iterations", (unsigned long long)iters);
-        batch = std::min<uint32_t>(batch * 2, 16);
-    }
+    for (uint32_t s0 = 0; s0 < p.spp; s0 += chunk) {
+        const uint32_t ns = std::min(chunk, p.spp - s0);
+        // Chunk start: empty queue 0, cursor at the chunk's first work item.
+        HIP_TRY(hipMemsetAsync(cnt, 0, offsetof(Counters, stats), stream));
+        const uint64_t w0 = (uint64_t)s0 * P;
+        // Pinned source, read when the copy executes: every earlier copy has
+        // completed (the previous chunk synchronised on later events).
+        ws.host_cursor[0] = w0;
+        HIP_TRY(hipMemcpyAsync(&cnt->cursor[1], ws.host_cursor, sizeof(uint64_t), hipMemcpyHostToDevice, stream));
+        ra.work_end = w0 + (uint64_t)ns * P;
+        sa.sample0 = s0;
+        // initial fill of queue 0 (survivors = 0 from the zeroed surv[0])
+        ra.q = q[0]; ra.surv = &cnt->surv[0]; ra.cursor_in = &cnt->cursor[1]; ra.cursor_out = &cnt->cursor[0];
+        ra.qn_out = &cnt->qn[0];
+        if ((st = mark(0, [&] { return launch_refill(ra, (uint32_t)C, stream); }))) return st;
 
-    if (timing) {
-        if ((st = get_event(ws, ev, &e0))) return st;
-        HIP_TRY(hipEventRecord(e0, stream));
-        timed.push_back({ev, 3});
-        ev += 2;
-    }
-    HIP_TRY(launch_resolve(ws.film, film_dev, (uint32_t)P, (uint32_t)k, p.spp, stream));
-    if (timing) {
-        if ((st = get_event(ws, ev - 1, &e1))) return st;
-        HIP_TRY(hipEventRecord(e1, stream));
+        // isect -> shade -> refill until the queue drains.  The live count is
+        // read back once per batch, one batch behind the launches; it never
+        // exceeds C, so a stale value is a safe grid size.
+        const uint64_t max_iters = ((uint64_t)ns * P * p.max_depth + C - 1) / C + p.max_depth + 64;
+        uint32_t known = (uint32_t)C;
+        uint64_t it = 0;
+        int cur = 0, pending = -1;
+        uint32_t batch = 4, nbatch = 0;
+        while (true) {
+            for (uint32_t b = 0; b < batch; b++) {
+                const int nx = 1 - cur;
+                ia.q = q[cur];
+                ia.count = &cnt->qn[cur];
+                if ((st = mark(1, [&] { return launch_isect_queue(ia, known, stream); }))) return st;
+                HIP_TRY(hipMemsetAsync(&cnt->surv[nx], 0, sizeof(uint32_t), stream));
+                sa.in = q[cur]; sa.out = q[nx];
+                sa.count_in = &cnt->qn[cur];
+                sa.count_out = &cnt->surv[nx];
+                if ((st = mark(2, [&] { return launch_shade(sa, known, stream); }))) return st;
+                ra.q = q[nx]; ra.surv = &cnt->surv[nx]; ra.cursor_in = &cnt->cursor[cur];
+                ra.cursor_out = &cnt->cursor[nx]; ra.qn_out = &cnt->qn[nx];
+                if ((st = mark(0, [&] { return launch_refill(ra, (uint32_t)C, stream); }))) return st;
+                cur = nx;
+                it++;
+            }
+            const int slot = (int)(nbatch++ & 1u);
+            HIP_TRY(hipMemcpyAsync(ws.host_counts + slot, &cnt->qn[cur], sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   stream));
+            HIP_TRY(hipEventRecord(ws.count_ev[slot], stream));
+            if (pending >= 0) {
+                HIP_TRY(hipEventSynchronize(ws.count_ev[pending]));
+                known = ws.host_counts[pending];
+                if (known == 0) break;
+            }
+            pending = slot;
+            if (it > max_iters)
+                return fail(SPT_ERR_HIP, "spt_render: queue did not drain after %llu iterations",
+                            (unsigned long long)it);
+            batch = std::min<uint32_t>(batch * 2, 16);
+        }
+        iters += it;
+        if ((st = mark(3, [&] {
+                 return launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
+                                       stream);
+             })))
+            return st;
     }
     unsigned long long hstats[3] = {0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(hstats, ws.stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(hstats, cnt->stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
     rs.continuations = hstats[1];
-    rs.regenerations = hstats[2];
+    rs.regenerations = hstats[2] > C ? hstats[2] - std::min<uint64_t>(C, P * p.spp) : 0;
     rs.iterations = iters;
     if (timing) {
         for (auto& tk : timed) {

@@ -154,38 +154,54 @@ __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o,
     q.tr[j] = tr; q.tg[j] = tg; q.tb[j] = tb;
 }
 
-// Entry e = s * P + p starts sample s of tile pixel p (s < k_eff).
-__global__ __launch_bounds__(256) void camera_init_kernel(CameraInitArgs a, uint32_t items) {
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= items) return;
-    const uint32_t s = e / a.P, p = e % a.P;
+// Refill: start work items [cursor, cursor + total) in queue slots
+// [surv, surv + total).  Work item w is sample w / P of tile pixel w % P, so a
+// refill hands consecutive lanes consecutive pixels of one sample (coherent
+// camera rays).  RNG: the pixel's PCG32 stream (main.cpp:376) advanced to the
+// sample's first draw, s * (4 + 2D) draws (main.cpp:395,396,413 per sample).
+__global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
+    const uint32_t surv = *a.surv;
+    const uint64_t cur = *a.cursor_in;
+    const uint64_t avail = a.work_end > cur ? a.work_end - cur : 0;
+    const uint32_t room = a.capacity - surv;
+    const uint32_t total = (uint32_t)(avail < room ? avail : room);
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) {
+        *a.cursor_out = cur + total;
+        *a.qn_out = surv + total;
+        if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
+    }
+    if (i >= total) return;
+    const uint64_t w = cur + i;
+    const uint32_t s = (uint32_t)(w / a.P);
+    const uint32_t p = (uint32_t)(w - (uint64_t)s * a.P);
     const uint32_t lx = p % a.W, ly = p / a.W;
     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
     const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
     Pcg32 rng;
     rng.seed(a.initstate, (uint64_t)gpix);                   // main.cpp:376
-    if (s) rng.state = pcg_apply(pcg_jump_coeffs((uint64_t)s * (4u + 2u * a.max_depth)), rng.state, rng.inc);
+    rng.state = pcg_apply(a.sample_jump[s], rng.state, rng.inc);
     V3 o, d;
     camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
-    store_path(a.q, e, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f);
+    store_path(a.q, surv + i, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f);  // main.cpp:391
 }
 
 // ----------------------------------------------------------------- shade
-// main.cpp:404-425 for one cast of every queued path, plus path regeneration
-// (a finished sample immediately starts the pixel's next sample in the same
-// lane) and ballot/mbcnt compaction of the survivors into the out queue
-// (one atomic per block).
+// main.cpp:404-425 for one cast of every queued path.  A path that ends
+// writes its one contribution (throughput x sky radiance on escape, else 0)
+// to sfilm[sample][c][pixel]; survivors are compacted into the out queue with
+// a wave ballot + mbcnt rank and one atomicAdd per block.
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
-    __shared__ uint32_t s_stats[3];
+    __shared__ uint32_t s_stats[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t i = blockIdx.x * kShadeBlock + tid;
     const uint32_t n = *a.count_in;
-    if (tid < 3) s_stats[tid] = 0;
+    if (tid < 2) s_stats[tid] = 0;
     __syncthreads();
 
-    bool emit = false, cont = false, regen = false;
+    bool emit = false;
     V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
     uint32_t pix = 0, nmeta = 0;
     uint64_t nrng = 0;
@@ -197,28 +213,25 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         const uint32_t sample = meta >> kMetaDepthBits;
         const int32_t slot = a.hit_slot[i];
         tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
-        const uint32_t lx = pix % a.W, ly = pix / a.W;
-        const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
-        const uint32_t gpix = gy * a.W + lx;
-        Pcg32 rng;
-        rng.state = a.in.rng[i];
-        rng.inc = ((uint64_t)gpix << 1u) | 1u;
         bool term = true;
-        uint32_t pairs = depth;  // scatter draw pairs consumed by this sample
+        float cr = 0.0f, cg = 0.0f, cb = 0.0f;
         if (slot < 0) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
-            const uint32_t fs = sample % a.k;
-            float* f = a.film + (size_t)fs * 3 * a.P + pix;
-            f[0] = f[0] + tr * a.env_r;
-            f[(size_t)a.P] = f[(size_t)a.P] + tg * a.env_g;
-            f[(size_t)2 * a.P] = f[(size_t)2 * a.P] + tb * a.env_b;
+            cr = tr * a.env_r;
+            cg = tg * a.env_g;
+            cb = tb * a.env_b;
         } else if (depth + 1 < a.max_depth) {
+            const uint32_t lx = pix % a.W, ly = pix / a.W;
+            const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
+            const uint32_t gpix = gy * a.W + lx;
+            Pcg32 rng;
+            rng.state = a.in.rng[i];
+            rng.inc = ((uint64_t)gpix << 1u) | 1u;
             const V3 o = v3(a.in.ox[i], a.in.oy[i], a.in.oz[i]);
             const V3 d = v3(a.in.dx[i], a.in.dy[i], a.in.dz[i]);
             const float t = a.hit_t[i], u = a.hit_u[i], v = a.hit_v[i];
             float xi_x, xi_y;
             draw2(rng, a.rng_order, xi_x, xi_y);               // main.cpp:413
-            pairs = depth + 1;
             const float4 m0 = a.sc.snrm[(size_t)slot * 3];
             const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
             const float4 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
@@ -246,7 +259,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
                 }
             }
             if (!term) {
-                emit = cont = true;
+                emit = true;
                 no = hp;                                          // main.cpp:423
                 nd = out;                                         // main.cpp:424
                 nmeta = meta + 1u;
@@ -255,15 +268,10 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
         // else: hit on the last cast — the path ends without contribution.
         if (term) {
-            const uint32_t next = sample + a.k;
-            if (next < a.spp) {
-                rng.state = pcg_apply(a.jumps[pairs], rng.state, rng.inc);
-                camera_ray(a.cam, rng, a.rng_order, lx, gy, no, nd);
-                emit = regen = true;
-                nmeta = next << kMetaDepthBits;
-                nrng = rng.state;
-                tr = tg = tb = 1.0f;                              // main.cpp:391
-            }
+            float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
+            f[0] = cr;
+            f[(size_t)a.P] = cg;
+            f[(size_t)2 * a.P] = cb;
         }
     }
 
@@ -271,12 +279,11 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     const uint64_t ball = __ballot(emit);
     const uint32_t rank =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
-    const uint64_t bc = __ballot(cont), br = __ballot(regen), bi = __ballot(i < n);
+    const uint64_t bi = __ballot(i < n);
     if (lane == 0) {
         s_wave_cnt[wave] = (uint32_t)__popcll(ball);
         atomicAdd(&s_stats[0], (uint32_t)__popcll(bi));
-        atomicAdd(&s_stats[1], (uint32_t)__popcll(bc));
-        atomicAdd(&s_stats[2], (uint32_t)__popcll(br));
+        atomicAdd(&s_stats[1], (uint32_t)__popcll(ball));
     }
     __syncthreads();
     if (tid == 0) {
@@ -290,22 +297,27 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         if (s_stats[0]) {
             atomicAdd(&a.stats[0], (unsigned long long)s_stats[0]);
             if (s_stats[1]) atomicAdd(&a.stats[1], (unsigned long long)s_stats[1]);
-            if (s_stats[2]) atomicAdd(&a.stats[2], (unsigned long long)s_stats[2]);
         }
     }
     __syncthreads();
     if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb);
 }
 
-// film[k][3][P] -> out[3][P] / spp  (main.cpp:429)
-__global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ film, float* __restrict__ out,
-                                                      uint32_t P, uint32_t k_eff, uint32_t spp) {
+// Per-pixel sum of the per-sample contributions in sample order
+// (film += ... once per sample, main.cpp:407), then film /= spp (main.cpp:429).
+// Chunks of samples carry the running sum in acc.
+__global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ sfilm, float* __restrict__ acc,
+                                                      float* __restrict__ out, uint32_t P, uint32_t nsamples,
+                                                      uint32_t first_chunk, uint32_t last_chunk, uint32_t spp) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= P) return;
     for (uint32_t c = 0; c < 3; c++) {
-        float sum = 0.0f;
-        for (uint32_t s = 0; s < k_eff; s++) sum = sum + film[((size_t)s * 3 + c) * P + p];
-        out[(size_t)c * P + p] = sum / (float)spp;
+        float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
+        for (uint32_t s = 0; s < nsamples; s++) sum = sum + sfilm[((size_t)s * 3 + c) * P + p];
+        if (last_chunk)
+            out[(size_t)c * P + p] = sum / (float)spp;
+        else
+            acc[(size_t)c * P + p] = sum;
     }
 }
 
@@ -374,15 +386,16 @@ hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_camera_init(const CameraInitArgs& a, uint32_t items, hipStream_t s) {
-    if (items == 0) return hipSuccess;
-    hipLaunchKernelGGL(camera_init_kernel, dim3(blocks_for(items, 256)), dim3(256), 0, s, a, items);
+hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s) {
+    hipLaunchKernelGGL(refill_kernel, dim3(blocks_for(grid_items > 0 ? grid_items : 1, 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_resolve(const float* film, float* out, uint32_t P, uint32_t k_eff, uint32_t spp, hipStream_t s) {
+hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
+                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, hipStream_t s) {
     if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(resolve_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, film, out, P, k_eff, spp);
+    hipLaunchKernelGGL(resolve_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sfilm, acc, out, P, nsamples,
+                       first_chunk, last_chunk, spp);
     return hipGetLastError();
 }
 

@@ -4,7 +4,7 @@
 // override them.
 //
 //   spt_render_cli [scene.obj] [-w W] [-h H] [-s spp] [-d casts] [-o out.pfm]
-//                  [--ppp k] [--rr depth] [--rng-x-first] [--device N]
+//                  [--wavefront paths] [--rr depth] [--rng-x-first] [--device N]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -33,7 +33,7 @@ int main(int argc, char** argv) {
         else if (a == "-s") p.spp = (uint32_t)std::atoi(next());
         else if (a == "-d") p.max_depth = (uint32_t)std::atoi(next());
         else if (a == "-o") out = next();
-        else if (a == "--ppp") p.paths_per_pixel = (uint32_t)std::atoi(next());
+        else if (a == "--wavefront") p.wavefront_paths = (uint32_t)std::atoi(next());
         else if (a == "--rr") p.rr_start_depth = (uint32_t)std::atoi(next());
         else if (a == "--rng-x-first") p.rng_order = SPT_RNG_X_FIRST;
         else if (a == "--device") device = std::atoi(next());

@@ -61,20 +61,27 @@ struct ShadeArgs {
     const int32_t* hit_slot;
     const float *hit_t, *hit_u, *hit_v;
     const uint32_t* count_in;
-    uint32_t* count_out;
-    float* film;              // [k][3][P]
-    unsigned long long* stats; // casts, continuations, regenerations
-    Camera cam;
-    uint32_t P, W, k, spp, max_depth, rr_start, rng_order;
+    uint32_t* count_out;        // survivors appended here (zeroed before the launch)
+    float* sfilm;               // [spp_chunk][3][P]: one contribution per (sample, pixel)
+    unsigned long long* stats;  // casts, continuations, regenerations
+    uint32_t P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     float env_r, env_g, env_b;
-    PcgJump jumps[kMaxDepthCasts + 1];  // indexed by scatter pairs consumed
 };
 
-struct CameraInitArgs {
+// Starts new paths in queue slots [*surv, capacity): work item w (sample-major:
+// sample = w / P, tile pixel = w % P) for w in [*cursor_in, W_total).
+struct RefillArgs {
     PathQueue q;
     Camera cam;
-    uint32_t P, W, k_eff, max_depth, rng_order;
+    const uint32_t* surv;       // survivors already in the queue
+    const uint64_t* cursor_in;
+    uint64_t* cursor_out;       // written by thread 0 only
+    uint32_t* qn_out;           // queue count for the next isect, thread 0 only
+    const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
+    unsigned long long* stats;
+    uint64_t work_end;          // W_total (work items of this chunk end here)
+    uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     uint64_t initstate;
 };
@@ -100,9 +107,9 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
 hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s);
-hipError_t launch_camera_init(const CameraInitArgs& a, uint32_t items, hipStream_t s);
-hipError_t launch_resolve(const float* film, float* out, uint32_t P, uint32_t k_eff, uint32_t spp,
-                          hipStream_t s);
+hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);
+hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
+                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, hipStream_t s);
 hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s);
 
 }  // namespace spt

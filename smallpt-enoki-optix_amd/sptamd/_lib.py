@@ -60,7 +60,7 @@ class RenderParams(ctypes.Structure):
     _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_depth", c_uint32),
                 ("camera", Camera),
                 ("tile_index", c_uint32), ("tile_count", c_uint32), ("rows_per_group", c_uint32),
-                ("paths_per_pixel", c_uint32), ("rr_start_depth", c_uint32), ("rng_order", c_uint32),
+                ("wavefront_paths", c_uint32), ("rr_start_depth", c_uint32), ("rng_order", c_uint32),
                 ("rng_initstate", c_uint64), ("env", c_float * 3), ("flags", c_uint32)]
 
 
@@ -92,6 +92,11 @@ class Mesh(ctypes.Structure):
 
 
 def _load() -> ctypes.CDLL:
+    # torch ships its own HIP runtime (SONAME libamdhip64.so.7).  Load it first
+    # so libspt.so binds to that one copy: loading libspt.so first would map the
+    # system runtime too and put two HIP runtimes in one process.
+    import torch  # noqa: F401
+
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libspt.so not built at {LIB_PATH}: run `make -C smallpt-enoki-optix_amd` "
                           "(or __graft_entry__.build()); there is no CPU fallback")

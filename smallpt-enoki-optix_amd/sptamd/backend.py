@@ -195,7 +195,7 @@ def reference_camera() -> dict:
 
 
 def make_params(width: int, height: int, spp: int, max_depth: int, camera: Optional[dict] = None,
-                tile_index: int = 0, tile_count: int = 1, rows_per_group: int = 1, paths_per_pixel: int = 0,
+                tile_index: int = 0, tile_count: int = 1, rows_per_group: int = 1, wavefront_paths: int = 0,
                 rr_start_depth: int = 1, rng_order: int = 0, env=(1.0, 1.0, 1.0), timing: bool = False,
                 rng_initstate: int = _lib.PCG32_DEFAULT_STATE) -> RenderParams:
     p = _lib.default_params()
@@ -208,7 +208,7 @@ def make_params(width: int, height: int, spp: int, max_depth: int, camera: Optio
     p.camera.fov_y = cam["fov_y"]
     p.camera.film_size_y = cam["film_size_y"]
     p.tile_index, p.tile_count, p.rows_per_group = tile_index, tile_count, rows_per_group
-    p.paths_per_pixel = paths_per_pixel
+    p.wavefront_paths = wavefront_paths
     p.rr_start_depth = rr_start_depth
     p.rng_order = rng_order
     p.rng_initstate = rng_initstate

@@ -2,8 +2,9 @@
 CPU oracle.  The reference's image is an escape count per pixel (albedo 1,
 sky radiance 1: SURVEY F6), so the film is an exact multiple of 1/spp and the
 GPU result must equal the oracle bit for bit.  Non-unit albedo (Russian
-roulette active) is compared with a stated tolerance when several samples of
-a pixel are in flight (different fp32 summation order), bitwise otherwise."""
+roulette active) is bitwise too: every path writes one contribution per
+(sample, pixel) and the resolve sums them in sample order, as the reference's
+film += ... does (main.cpp:407)."""
 import numpy as np
 import pytest
 import torch
@@ -62,12 +63,12 @@ def test_render_rng_x_first(gscene, oscene):
     assert not np.array_equal(got, other)
 
 
-@pytest.mark.parametrize("ppp", [1, 2, 3, 7])
-def test_paths_in_flight_invariance(gscene, ppp):
-    base, _ = gpu_render(gscene, 48, 40, 7, 4, paths_per_pixel=1)
-    got, st = gpu_render(gscene, 48, 40, 7, 4, paths_per_pixel=ppp)
-    np.testing.assert_array_equal(got, base)
-    assert st["paths_in_flight"] == 48 * 40 * ppp
+@pytest.mark.parametrize("wf", [1, 64, 1000, 48 * 40 * 7, 10**7])
+def test_wavefront_size_invariance(gscene, oscene, wf):
+    got, st = gpu_render(gscene, 48, 40, 7, 4, wavefront_paths=wf)
+    ref, _ = oracle_render(oscene, 48, 40, 7, 4)
+    np.testing.assert_array_equal(got, ref)
+    assert st["paths_in_flight"] == min(wf, 48 * 40 * 7)
 
 
 @pytest.mark.parametrize("tiles,rpg", [(2, 1), (3, 5), (8, 8), (5, 64)])
@@ -95,15 +96,15 @@ def test_albedo_and_russian_roulette(mesh):
                        [0.4, 0.4, 0.4]], np.float32)
     s.backend.set_albedo(albedo)
     osc = O.OracleScene(mesh, albedo=albedo)
-    got, st = gpu_render(s, 40, 30, 6, 6, paths_per_pixel=1, rr_start_depth=2)
+    got, st = gpu_render(s, 40, 30, 6, 6, rr_start_depth=2)
     ref, casts = oracle_render(osc, 40, 30, 6, 6, rr_start_depth=2)
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts
-    # several samples of a pixel in flight: same estimate, different fp32 summation order
-    got3, _ = gpu_render(s, 40, 30, 6, 6, paths_per_pixel=3, rr_start_depth=2)
-    np.testing.assert_allclose(got3, ref, rtol=1e-6, atol=1e-6)
+    # a small wavefront: many refills, same per-sample summation order, same bits
+    got3, _ = gpu_render(s, 40, 30, 6, 6, wavefront_paths=500, rr_start_depth=2)
+    np.testing.assert_array_equal(got3, ref)
     # roulette disabled = the reference estimator (no RR): still exact
-    got_norr, _ = gpu_render(s, 40, 30, 6, 6, paths_per_pixel=1, rr_start_depth=99)
+    got_norr, _ = gpu_render(s, 40, 30, 6, 6, rr_start_depth=99)
     ref_norr, _ = oracle_render(osc, 40, 30, 6, 6, rr_start_depth=99)
     np.testing.assert_array_equal(got_norr, ref_norr)
 
