@@ -83,6 +83,7 @@ def main():
 
     import sptamd
     from sptamd import scenes
+    from sptamd.distributed import TileGather
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,25 +108,14 @@ def main():
     R = args.rows_per_group
     params = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
                                 wavefront_paths=args.wavefront, timing=True)
-    rows_all = [sptamd.tile_rows(H, r, world, R) for r in range(world)]
-    max_rows = max(len(r) for r in rows_all)
     dev = torch.device("cuda", local)
-    tile = torch.zeros((3, max_rows, W), dtype=torch.float32, device=dev)
-    my_rows = len(rows_all[rank])
-    gather_list = [torch.empty_like(tile) for _ in range(world)] if rank == 0 and world > 1 else None
-    image = torch.empty((3, H, W), dtype=torch.float32, device=dev) if rank == 0 else None
-    row_index = [torch.as_tensor(r, device=dev) for r in rows_all] if rank == 0 else None
+    tg = TileGather(H, W, rank, world, R, dev)
+    film = tg.tile_view()
     stream = torch.cuda.current_stream()
 
     def step():
-        _, st = scene.render(params, film=tile, stream=stream)
-        if world > 1:
-            dist.gather(tile, gather_list, dst=0)
-            if rank == 0:
-                for r in range(world):
-                    image[:, row_index[r], :] = gather_list[r][:, :len(rows_all[r]), :]
-        else:
-            image.copy_(tile[:, :H, :])
+        _, st = scene.render(params, film=film, stream=stream)
+        tg.gather()
         return st
 
     for _ in range(args.warmup):
@@ -191,7 +181,7 @@ def main():
             "bvh": {k: sstats[k] for k in ("nodes", "max_depth", "build_ms", "sah_cost")},
         }
         if args.save:
-            np.save(args.save, image.cpu().numpy())
+            np.save(args.save, tg.image.cpu().numpy())
         if world == 1 and not args.no_cpu_baseline:
             mesh = scenes.load_obj(obj)
             rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads)

@@ -130,3 +130,25 @@ def test_headline_config_properties(gscene, oscene):
     np.testing.assert_array_equal(got[:, rows, :], ref)
     assert st["paths"] == w * h * spp
     assert st["ray_casts"] >= st["paths"]
+
+
+def test_gpu_matches_committed_golden():
+    """GPU vs the committed oracle vectors (tests/golden/oracle_small.npz)."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_small.npz"))
+    m = scenes.mitsuba_synth(detail=0.1)
+    s = sptamd.Scene()
+    s.add_arrays(m)
+    s.commit(0)
+    np.testing.assert_array_equal(gpu_render(s, 32, 24, 4, 4)[0], g["film_32x24_4spp_d4"])
+    np.testing.assert_array_equal(gpu_render(s, 32, 24, 4, 4, rng_order=1)[0], g["film_32x24_4spp_d4_xfirst"])
+    np.testing.assert_array_equal(gpu_render(s, 16, 16, 100, 2)[0], g["film_16x16_100spp_d2"])
+    rays = sptamd.Ray3.make(g["isect_o"], g["isect_d"])
+    tri, t, u, v = s.backend.intersect_raw(rays)
+    torch.cuda.synchronize()
+    tri = tri.cpu().numpy()
+    np.testing.assert_array_equal(tri, g["isect_tri"])
+    h = tri >= 0
+    np.testing.assert_array_equal(t.cpu().numpy()[h], g["isect_t"][h])
+    s.backend.set_albedo(g["albedo"])
+    np.testing.assert_array_equal(gpu_render(s, 20, 16, 6, 6, rr_start_depth=2)[0], g["film_albedo_rr2"])

@@ -1,0 +1,146 @@
+"""Host-side checks without a GPU: the C ABI library loads and exports every
+function include/spt.h declares (no compute calls), the reference defaults,
+the OBJ reader's tinyobj index semantics (main.cpp:141-251), the PFM writer
+(fimage.h:33-58) and error behaviour."""
+import ctypes
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+
+import sptamd
+from sptamd import _lib, scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "spt.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(spt_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_symbols_exported():
+    names = declared_functions()
+    assert len(names) >= 15
+    assert sorted(_lib.EXPORTED) == names
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_version_and_errors_without_gpu():
+    assert b"gfx950" in _lib.lib.spt_version()
+    # invalid arguments are rejected before any device work
+    st = _lib.lib.spt_scene_create(None, None, 0, 0, None, None, 0, None, None, 0, None, None)
+    assert st == 1 and b"NULL" in _lib.lib.spt_last_error()
+    with pytest.raises(sptamd.SptError):
+        sptamd.check(_lib.lib.spt_render(None, None, None, None, None), "spt_render")
+
+
+def test_default_params_are_the_reference_main():
+    p = sptamd.default_params()
+    assert (p.width, p.height, p.spp, p.max_depth) == (512, 512, 100, 2)          # main.cpp:357-361
+    assert list(p.camera.look_from) == [0.0, np.float32(3.03), 5.0]              # main.cpp:383
+    assert list(p.camera.look_at) == [0.0, np.float32(0.03), 0.0]
+    assert p.camera.lens_radius == 0.0 and p.camera.focal_dist == 1.0
+    assert p.camera.fov_y == np.float32(np.float32(40.0 / 180.0) * np.float32(np.pi))
+    assert p.camera.film_size_y == np.float32(0.035)                              # pinhole.h:11
+    assert p.rng_initstate == 0x853C49E6748FEA9B                                   # main.cpp:376
+    assert list(p.env) == [1.0, 1.0, 1.0] and p.rng_order == 0
+
+
+def _write(path, text):
+    with open(path, "w") as f:
+        f.write(text)
+
+
+def test_obj_loader_semantics(tmp_path):
+    _write(tmp_path / "m.mtl", "newmtl red\nKd 0.9 0.1 0.1\n\nnewmtl blue\nKd 0.1 0.1 0.9\n")
+    _write(tmp_path / "a.obj", """# test
+mtllib m.mtl
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+v 0 0 1
+vn 0 0 1
+vn 0 1 0
+vt 0 0
+vt 1 0
+vt 1 1
+f 1 2 3
+usemtl blue
+f 1//1 3//1 4//2
+usemtl red
+f 1/1/1 2/2/1 3/3/2 4/1/2
+usemtl nope
+f -1 -2 -3
+""")
+    m = scenes.load_obj(str(tmp_path / "a.obj"))
+    np.testing.assert_array_equal(m["pos_tri"], [[0, 1, 2], [0, 2, 3], [0, 1, 2], [0, 2, 3], [4, 3, 2]])
+    np.testing.assert_array_equal(m["nrm_tri"], [[-1, -1, -1], [0, 0, 1], [0, 0, 1], [0, 1, 1], [-1, -1, -1]])
+    np.testing.assert_array_equal(m["tc_tri"], [[-1, -1, -1], [-1, -1, -1], [0, 1, 2], [0, 2, 0], [-1, -1, -1]])
+    # obj material id + 1 (main.cpp:185): none -> 0, blue (index 1) -> 2, red (0) -> 1, unknown -> 0
+    np.testing.assert_array_equal(m["mat_id"], [0, 2, 1, 1, 0])
+    np.testing.assert_allclose(m["kd"], [[1, 1, 1], [0.9, 0.1, 0.1], [0.1, 0.1, 0.9]])
+    assert m["pos"].shape == (5, 3) and m["nrm"].shape == (2, 3) and m["tc"].shape == (3, 2)
+
+
+def test_obj_loader_errors(tmp_path):
+    mesh = _lib.Mesh()
+    assert _lib.lib.spt_obj_load(str(tmp_path / "missing.obj").encode(), ctypes.byref(mesh)) == 5
+    _write(tmp_path / "bad.obj", "v 0 0 0\nv 1 0 0\nf 1 2 7\n")
+    assert _lib.lib.spt_obj_load(str(tmp_path / "bad.obj").encode(), ctypes.byref(mesh)) == 1
+
+
+def test_generated_scene_roundtrip(tmp_path):
+    m = scenes.mitsuba_synth(detail=0.1)
+    path = str(tmp_path / "s.obj")
+    scenes.write_obj(path, m)
+    l = scenes.load_obj(path)
+    for k in ("pos_tri", "nrm_tri", "mat_id"):
+        np.testing.assert_array_equal(l[k], m[k])
+    for k in ("pos", "nrm", "kd"):
+        np.testing.assert_array_equal(l[k], m[k].astype(np.float32))
+
+
+def test_pfm_writer(tmp_path):
+    h, w = 3, 4
+    film = np.arange(3 * h * w, dtype=np.float32).reshape(3, h, w)
+    path = str(tmp_path / "x.pfm")
+    sptamd.write_pfm(path, film)
+    data = open(path, "rb").read()
+    header = b"PF\n%d %d\n-1\n" % (w, h)
+    assert data.startswith(header)
+    px = np.frombuffer(data[len(header):], dtype="<f4").reshape(h, w, 3)
+    # rows bottom-up, interleaved RGB (fimage.h:46-55)
+    np.testing.assert_array_equal(px, film.transpose(1, 2, 0)[::-1])
+    assert struct.calcsize("<f") * 3 * h * w == len(data) - len(header)
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes layouts == what a C compiler makes of include/spt.h."""
+    import subprocess
+    structs = {"spt_render_params": _lib.RenderParams, "spt_render_stats": _lib.RenderStats,
+               "spt_scene_stats": _lib.SceneStats, "spt_rays": _lib.Rays, "spt_hits": _lib.Hits,
+               "spt_hit_info": _lib.HitInfo, "spt_camera": _lib.Camera, "spt_mesh": _lib.Mesh}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, ct in structs.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in ct._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for line in filter(None, out):
+        cname, field, val = line.split()
+        ct = structs[cname]
+        got = ctypes.sizeof(ct) if field == "sizeof" else getattr(ct, field).offset
+        assert got == int(val), (cname, field, got, val)

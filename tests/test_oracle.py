@@ -1,0 +1,237 @@
+"""CPU oracle pins (no GPU): published PCG32 known answers, formula-derived
+camera known answers, analytic scenes, BVH vs brute force, and
+the committed golden vectors (tests/golden/make_golden.py)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from sptamd import scenes
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_small.npz")
+MULT = 0x5851F42D4C957F2D
+M64 = (1 << 64) - 1
+
+
+def test_pcg32_canonical_kat():
+    # pcg32 reference implementation, pcg32_srandom_r(42, 54): the published demo output
+    got = O.pcg32_seq(42, 54, 6)
+    assert [f"{x:08x}" for x in got] == ["a15c02b7", "7b47f409", "ba1d3330", "83d2f293", "bfa4784b", "cbed606e"]
+
+
+@pytest.mark.parametrize("seq,expect", [
+    (0, ["69c87837", "6694bd1c", "a37b7ac6", "572d246c"]),
+    (1, ["73c29fdb", "fbaa1ff7", "db022af6", "12d7398c"]),
+    (1023, ["0a82b6cb", "7666067b", "68efb589", "a03cf93b"]),
+])
+def test_pcg32_reference_seeding(seq, expect):
+    # main.cpp:376 — initstate PCG32_DEFAULT_STATE, initseq = pixel index
+    assert [f"{x:08x}" for x in O.pcg32_seq(O.PCG32_DEFAULT_STATE, seq, 4)] == expect
+
+
+def test_next_float32_mapping():
+    u = O.pcg32_seq(O.PCG32_DEFAULT_STATE, 7, 64)
+    f = O.pcg32_floats(O.PCG32_DEFAULT_STATE, 7, 64)
+    expect = ((u >> 9) | 0x3F800000).astype(np.uint32).view(np.float32) - np.float32(1.0)
+    np.testing.assert_array_equal(f, expect)
+    assert f.min() >= 0.0 and f.max() < 1.0
+
+
+def _jump(n):
+    """Restatement of spt_math.h pcg_jump_coeffs (used by the GPU refill)."""
+    am, aa, cm, ca = 1, 0, MULT, 1
+    while n:
+        if n & 1:
+            am, aa = (am * cm) & M64, (aa * cm + ca) & M64
+        ca = ((cm + 1) * ca) & M64
+        cm = (cm * cm) & M64
+        n >>= 1
+    return am, aa
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 20, 68, 4 * 68 + 2, 1000])
+def test_pcg32_jump_ahead(n):
+    # seeding state, then n LCG steps == one affine jump
+    inc = (12345 << 1) | 1
+    st = 0
+    st = (st * MULT + inc) & M64
+    st = (st + O.PCG32_DEFAULT_STATE) & M64
+    st = (st * MULT + inc) & M64
+    s = st
+    for _ in range(n):
+        s = (s * MULT + inc) & M64
+    am, aa = _jump(n)
+    assert (am * st + aa * inc) & M64 == s
+
+
+def test_camera_known_answers():
+    p = O.reference_params(1024, 1024, 1, 1)
+    o, d, basis = O.camera_ray(p, 0, 0, [0, 0, 0, 0])
+    np.testing.assert_allclose(basis[0], [-1, 0, 0], atol=1e-6)
+    np.testing.assert_allclose(basis[1], [0, 0.857493, -0.514496], atol=1e-6)
+    np.testing.assert_allclose(basis[2], [0, -0.514496, -0.857493], atol=1e-6)
+    np.testing.assert_array_equal(o, np.array([0.0, 3.03, 5.0], np.float32))  # lens radius 0
+    np.testing.assert_allclose(d, [-0.323616, -0.179954, -0.928919], atol=2e-6)
+    _, d2, _ = O.camera_ray(p, 512, 512, [0, 0, 0, 0])
+    np.testing.assert_allclose(d2, [0, -0.514496, -0.857493], atol=2e-6)
+
+
+def test_sincos_accuracy():
+    xs = np.linspace(-4 * math.pi, 4 * math.pi, 20001).astype(np.float32)
+    err = 0.0
+    for x in xs[::7]:
+        s, c = O.sincos(float(x))
+        err = max(err, abs(s - math.sin(float(x))), abs(c - math.cos(float(x))))
+    assert err < 3e-7
+
+
+def test_cosine_hemisphere():
+    g = (np.arange(64) + 0.5) / 64
+    ys, norms = [], []
+    for a in g:
+        for b in g[::4]:
+            v = O.cosine_hemisphere(float(a), float(b))
+            ys.append(v[1])
+            norms.append(np.linalg.norm(v))
+            assert v[1] == np.float32(math.sqrt(np.float32(a)))  # mapping.h:10
+    np.testing.assert_allclose(norms, 1.0, atol=1e-6)
+    assert abs(np.mean(ys) - 2.0 / 3.0) < 2e-3                 # E[cos] under cos/pi
+
+
+def test_disk_from_square():
+    for a in np.linspace(0.0, 0.999, 37):
+        for b in np.linspace(0.001, 0.999, 41):
+            p = O.disk_from_square(float(a), float(b))
+            assert np.hypot(*p) <= 1.0 + 1e-6
+    np.testing.assert_allclose(np.hypot(*O.disk_from_square(0.0, 0.5)), 1.0, atol=1e-6)
+
+
+def test_frame_unit_normal_orthonormal():
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        n = rng.normal(size=3).astype(np.float32)
+        n /= np.linalg.norm(n)
+        y = O.frame_to_world(n, [0, 1, 0])
+        np.testing.assert_allclose(y, n, atol=1e-7)
+        bx = O.frame_to_world(n, [1, 0, 0])
+        bz = O.frame_to_world(n, [0, 0, 1])
+        m = np.stack([bx, y, bz])
+        np.testing.assert_allclose(m @ m.T, np.eye(3), atol=2e-6)
+
+
+def _mt64(o, d, v0, v1, v2):
+    """float64 Moller-Trumbore reference."""
+    e1, e2 = v1 - v0, v2 - v0
+    p = np.cross(d, e2)
+    det = e1 @ p
+    if abs(det) < 1e-300:
+        return None
+    tv = o - v0
+    u = (tv @ p) / det
+    q = np.cross(tv, e1)
+    v = (d @ q) / det
+    t = (e2 @ q) / det
+    return t, u, v
+
+
+def test_watertight_triangle_vs_float64():
+    rng = np.random.default_rng(3)
+    n = 3000
+    tri = rng.normal(size=(n, 3, 3)).astype(np.float32)
+    mesh = {"pos": tri.reshape(-1, 3), "pos_tri": np.arange(3 * n, dtype=np.int32).reshape(-1, 3)}
+    sc = O.OracleScene(mesh, use_bvh=False)
+    agree = 0
+    for k in range(n):
+        o = rng.normal(size=3).astype(np.float32) * 3
+        target = tri[k].mean(0) + rng.normal(size=3).astype(np.float32) * 0.3
+        d = (target - o).astype(np.float32)
+        single = O.OracleScene({"pos": tri[k], "pos_tri": np.array([[0, 1, 2]], np.int32)}, use_bvh=False)
+        hid, t, u, v = single.intersect(o.reshape(3, 1), d.reshape(3, 1), tmin=np.zeros(1, np.float32))
+        ref = _mt64(o.astype(np.float64), d.astype(np.float64), *tri[k].astype(np.float64))
+        inside = ref is not None and ref[1] >= 0 and ref[2] >= 0 and ref[1] + ref[2] <= 1 and ref[0] >= 0
+        margin = ref is not None and min(abs(ref[1]), abs(ref[2]), abs(1 - ref[1] - ref[2])) < 1e-4
+        if margin:
+            continue
+        assert (hid[0] == 0) == inside
+        if inside:
+            np.testing.assert_allclose(t[0], ref[0], rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose([u[0], v[0]], [ref[1], ref[2]], atol=1e-5)
+        agree += 1
+    assert agree > 2500
+    del sc
+
+
+def test_bvh_equals_bruteforce():
+    mesh = scenes.mitsuba_synth(detail=0.1)
+    g = np.load(GOLDEN)
+    o, d = g["isect_o"], g["isect_d"]
+    a = O.OracleScene(mesh, use_bvh=True).intersect(o, d)
+    b = O.OracleScene(mesh, use_bvh=False).intersect(o, d)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    assert (a[0] >= 0).sum() > 1000
+
+
+def test_golden_vectors():
+    g = np.load(GOLDEN)
+    for s, row in zip(g["pcg_seeds"], g["pcg_u32"]):
+        np.testing.assert_array_equal(O.pcg32_seq(O.PCG32_DEFAULT_STATE, int(s), 32), row)
+    mesh = scenes.mitsuba_synth(detail=0.1)
+    sc = O.OracleScene(mesh)
+    tri, t, u, v = sc.intersect(g["isect_o"], g["isect_d"])
+    np.testing.assert_array_equal(tri, g["isect_tri"])
+    h = tri >= 0
+    for a, b in ((t, g["isect_t"]), (u, g["isect_u"]), (v, g["isect_v"])):
+        np.testing.assert_array_equal(a[h], b[h])
+    np.testing.assert_array_equal(sc.render(O.reference_params(32, 24, 4, 4))[0], g["film_32x24_4spp_d4"])
+    np.testing.assert_array_equal(sc.render(O.reference_params(32, 24, 4, 4, rng_order=1))[0],
+                                  g["film_32x24_4spp_d4_xfirst"])
+    np.testing.assert_array_equal(sc.render(O.reference_params(16, 16, 100, 2))[0], g["film_16x16_100spp_d2"])
+    alb = O.OracleScene(mesh, albedo=g["albedo"])
+    np.testing.assert_array_equal(alb.render(O.reference_params(20, 16, 6, 6, rr_start_depth=2))[0],
+                                  g["film_albedo_rr2"])
+
+
+def _big_plane(y=-1.0, half=100.0):
+    pos = np.array([[-half, y, -half], [half, y, -half], [half, y, half], [-half, y, half]], np.float32)
+    return {"pos": pos, "pos_tri": np.array([[0, 1, 2], [0, 2, 3]], np.int32),
+            "nrm": np.array([[0, 1, 0]], np.float32), "nrm_tri": np.zeros((2, 3), np.int32)}
+
+
+def test_analytic_plane():
+    """Camera above a plane wide enough to fill the view (half-size 100: at
+    1e4 the fp32 hit points drift ~1e-3 off the plane and re-hit it), looking
+    down: every camera
+    ray hits it; a bounce leaves upward and always escapes.  So with one cast
+    no path escapes (image 0) and with >= 2 casts every path does (image 1)."""
+    sc = O.OracleScene(_big_plane())
+    f1, casts1 = sc.render(O.reference_params(24, 24, 3, 1))
+    assert np.all(f1 == 0.0) and casts1 == 24 * 24 * 3
+    f3, casts3 = sc.render(O.reference_params(24, 24, 3, 3))
+    assert np.all(f3 == 1.0) and casts3 == 2 * 24 * 24 * 3
+
+
+def test_analytic_closed_box():
+    """A closed box around the camera: nothing escapes, at any depth."""
+    c = np.array([[x, y, z] for x in (-20, 20) for y in (-20, 20) for z in (-20, 20)], np.float32)
+    quads = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    tris = np.array([t for a, b, cc, d in quads for t in ((a, b, cc), (a, cc, d))], np.int32)
+    # inward normals: the bounce hemisphere follows the shading normal, unflipped (coordframe.h:17-30)
+    nrm = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float32)
+    nt = np.repeat(np.arange(6, dtype=np.int32), 2)[:, None].repeat(3, 1)
+    sc = O.OracleScene({"pos": c, "pos_tri": tris, "nrm": nrm, "nrm_tri": nt})
+    f, casts = sc.render(O.reference_params(16, 16, 2, 5))
+    assert np.all(f == 0.0) and casts == 16 * 16 * 2 * 5
+
+
+def test_film_is_escape_fraction():
+    """Albedo 1, sky 1: every pixel is an exact count / spp, R=G=B."""
+    sc = O.OracleScene(scenes.mitsuba_synth(detail=0.1))
+    f, _ = sc.render(O.reference_params(32, 32, 7, 4))
+    np.testing.assert_array_equal(f[0], f[1])
+    np.testing.assert_array_equal(f[0], f[2])
+    counts = f[0] * np.float32(7)
+    np.testing.assert_allclose(counts, np.round(counts), atol=1e-5)
+    assert 0.0 < f.mean() < 1.0
