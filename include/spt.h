@@ -75,7 +75,8 @@ enum {
 };
 
 enum {
-    SPT_FLAG_TIMING = 1u  /* record HIP events around every isect/shade launch */
+    SPT_FLAG_TIMING = 1u,          /* record HIP events around every isect/shade launch */
+    SPT_FLAG_TRAVERSAL_STATS = 2u  /* count node visits / triangle tests (slower variant) */
 };
 
 /* The render loop of main.cpp:354-429 plus the tile/wavefront knobs. */
@@ -105,6 +106,10 @@ typedef struct spt_render_stats {
     uint32_t tile_rows;
     double isect_ms, shade_ms, camera_ms, resolve_ms; /* SPT_FLAG_TIMING only (camera = refills) */
     double total_ms;            /* host wall time of the call (includes final sync) */
+    uint64_t isect_nodes;       /* SPT_FLAG_TRAVERSAL_STATS: inner nodes visited (all lanes) */
+    uint64_t isect_tris;        /*   triangle tests */
+    uint64_t isect_lane_steps;  /*   traversal loop iterations summed over lanes */
+    uint64_t isect_wave_steps;  /*   traversal loop iterations summed over waves */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

@@ -72,6 +72,7 @@ struct Counters {
     uint32_t surv[2];    // survivors appended by shade
     uint64_t cursor[2];  // next work item (double-buffered across refills)
     unsigned long long stats[3];  // casts, continuations, camera rays started
+    unsigned long long trav[4];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps
 };
 
 struct Workspace {
@@ -505,6 +506,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     ia.sc = sc->dev();
     ia.hit_slot = hit_slot; ia.hit_t = hit_t; ia.hit_u = hit_u; ia.hit_v = hit_v;
     ia.max_depth = p.max_depth;
+    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
+    ia.trav_stats = trav_stats ? cnt->trav : nullptr;
     ShadeArgs sa;
     sa.sc = sc->dev();
     sa.hit_slot = hit_slot; sa.hit_t = hit_t; sa.hit_u = hit_u; sa.hit_v = hit_v;
@@ -552,7 +555,11 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
                 const int nx = 1 - cur;
                 ia.q = q[cur];
                 ia.count = &cnt->qn[cur];
-                if ((st = mark(1, [&] { return launch_isect_queue(ia, known, stream); }))) return st;
+                if ((st = mark(1, [&] {
+                         return trav_stats ? launch_isect_queue_stats(ia, known, stream)
+                                           : launch_isect_queue(ia, known, stream);
+                     })))
+                    return st;
                 HIP_TRY(hipMemsetAsync(&cnt->surv[nx], 0, sizeof(uint32_t), stream));
                 sa.in = q[cur]; sa.out = q[nx];
                 sa.count_in = &cnt->qn[cur];
@@ -586,13 +593,17 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
              })))
             return st;
     }
-    unsigned long long hstats[3] = {0, 0, 0};
+    unsigned long long hstats[7] = {0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(hstats, cnt->stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
     rs.continuations = hstats[1];
     rs.regenerations = hstats[2] > C ? hstats[2] - std::min<uint64_t>(C, P * p.spp) : 0;
     rs.iterations = iters;
+    rs.isect_nodes = hstats[3];
+    rs.isect_tris = hstats[4];
+    rs.isect_lane_steps = hstats[5];
+    rs.isect_wave_steps = hstats[6];
     if (timing) {
         for (auto& tk : timed) {
             float ms = 0.0f;

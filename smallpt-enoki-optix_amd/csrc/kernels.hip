@@ -4,6 +4,8 @@
 //
 // Replaces wavefront_isect.cu:36-112 (OptiX raygen / closest-hit / miss) and
 // the Enoki-JIT bounce loop body main.cpp:385-426.
+#include <type_traits>
+
 #include "spt_internal.h"
 
 namespace spt {
@@ -20,8 +22,21 @@ struct TraceHit {
 // Closest hit: smallest t, ties broken toward the smaller original triangle
 // id so the answer does not depend on the tree.  anyhit: stop at the first
 // accepted triangle (OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
+struct NoStats {
+    __device__ void node() {}
+    __device__ void tri() {}
+    __device__ void step() {}
+};
+struct TravStats {
+    uint32_t nodes = 0, tris = 0, steps = 0;
+    __device__ void node() { nodes++; }
+    __device__ void tri() { tris++; }
+    __device__ void step() { steps++; }
+};
+
+template <typename Stats = NoStats>
 __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
-                                          bool anyhit, uint32_t* __restrict__ stk) {
+                                          bool anyhit, uint32_t* __restrict__ stk, Stats& stats) {
     TraceHit h;
     h.slot = -1;
     h.id = 0xffffffffu;
@@ -36,7 +51,9 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
     int32_t node = 0;
     uint32_t sp = 0;
     while (true) {
+        stats.step();
         if (node >= 0) {
+            stats.node();
             const float4* np = nodes + (size_t)node * 4;
             const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
             const float a0 = (n0.x - o.x) * ix, a1 = (n0.y - o.x) * ix;
@@ -70,6 +87,7 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
             const uint32_t code = ~(uint32_t)node;
             const uint32_t first = code >> 3, cnt = (code & 7u) + 1u;
             for (uint32_t i = 0; i < cnt; i++) {
+                stats.tri();
                 const uint32_t s = first + i;
                 const float4 t0 = tris[(size_t)s * 3], t1 = tris[(size_t)s * 3 + 1], t2 = tris[(size_t)s * 3 + 2];
                 float t, u, v;
@@ -97,6 +115,7 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
 // Wavefront isect over the path queue: one lane per queued ray.  The last
 // cast of a path only needs a yes/no answer (a miss is the only thing that
 // contributes, main.cpp:407), so it runs as an any-hit query.
+template <bool kStats>
 __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
@@ -106,7 +125,17 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
     const V3 d = v3(a.q.dx[i], a.q.dy[i], a.q.dz[i]);
     const uint32_t depth = a.q.meta[i] & ((1u << kMetaDepthBits) - 1u);
     const bool anyhit = depth + 1 >= a.max_depth;
-    const TraceHit h = trace(a.sc, o, d, kRayTmin, kRayTmax, anyhit, lds_stack + threadIdx.x);
+    typename std::conditional<kStats, TravStats, NoStats>::type st;
+    const TraceHit h = trace(a.sc, o, d, kRayTmin, kRayTmax, anyhit, lds_stack + threadIdx.x, st);
+    if constexpr (kStats) {
+        uint32_t wmax = st.steps;
+        for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off));
+        atomicAdd(&a.trav_stats[0], (unsigned long long)st.nodes);
+        atomicAdd(&a.trav_stats[1], (unsigned long long)st.tris);
+        atomicAdd(&a.trav_stats[2], (unsigned long long)st.steps);
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
+            atomicAdd(&a.trav_stats[3], (unsigned long long)wmax);
+    }
     a.hit_slot[i] = h.slot;
     a.hit_t[i] = h.t;
     a.hit_u[i] = h.u;
@@ -123,7 +152,8 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     const V3 o = v3(a.ox[i], a.oy[i], a.oz[i]);
     const V3 d = v3(a.dx[i], a.dy[i], a.dz[i]);
     const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
-    const TraceHit h = trace(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x);
+    NoStats st;
+    const TraceHit h = trace(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x, st);
     if (h.slot < 0) {
         a.tri_id[i] = -1;
         return;
@@ -369,7 +399,16 @@ static inline uint32_t blocks_for(uint32_t items, uint32_t block) { return (item
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
     const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
-    hipLaunchKernelGGL(isect_queue_kernel, dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
+    hipLaunchKernelGGL(isect_queue_kernel<false>, dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock), lds,
+                       s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+    if (grid_items == 0) return hipSuccess;
+    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
+    hipLaunchKernelGGL(isect_queue_kernel<true>, dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock), lds,
+                       s, a);
     return hipGetLastError();
 }
 

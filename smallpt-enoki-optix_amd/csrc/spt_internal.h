@@ -42,6 +42,7 @@ struct IsectQueueArgs {
     int32_t* hit_slot;
     float *hit_t, *hit_u, *hit_v;
     uint32_t max_depth;
+    unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
 };
 
 struct IsectPublicArgs {
@@ -105,6 +106,7 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
+hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
 hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);

@@ -17,6 +17,7 @@ SPT_OK = 0
 SPT_RNG_Y_FIRST = 0
 SPT_RNG_X_FIRST = 1
 SPT_FLAG_TIMING = 1
+SPT_FLAG_TRAVERSAL_STATS = 2
 PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
 
 # Every function include/spt.h declares (the CPU test checks they are exported).
@@ -69,7 +70,9 @@ class RenderStats(ctypes.Structure):
                 ("regenerations", c_uint64), ("iterations", c_uint64),
                 ("paths_in_flight", c_uint32), ("tile_rows", c_uint32),
                 ("isect_ms", c_double), ("shade_ms", c_double), ("camera_ms", c_double),
-                ("resolve_ms", c_double), ("total_ms", c_double)]
+                ("resolve_ms", c_double), ("total_ms", c_double),
+                ("isect_nodes", c_uint64), ("isect_tris", c_uint64), ("isect_lane_steps", c_uint64),
+                ("isect_wave_steps", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
