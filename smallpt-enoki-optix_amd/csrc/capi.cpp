@@ -73,6 +73,8 @@ struct Counters {
     uint64_t cursor[2];  // next work item (double-buffered across refills)
     unsigned long long stats[3];  // casts, continuations, camera rays started
     unsigned long long trav[4];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps
+    uint32_t isect_next;          // persistent isect work counter (zeroed by each refill)
+    uint32_t pad;
 };
 
 struct Workspace {
@@ -508,6 +510,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     ia.max_depth = p.max_depth;
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
     ia.trav_stats = trav_stats ? cnt->trav : nullptr;
+    ia.next = &cnt->isect_next;
     ShadeArgs sa;
     sa.sc = sc->dev();
     sa.hit_slot = hit_slot; sa.hit_t = hit_t; sa.hit_u = hit_u; sa.hit_v = hit_v;
@@ -524,6 +527,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     ra.capacity = (uint32_t)C; ra.P = (uint32_t)P; ra.W = p.width; ra.rng_order = p.rng_order;
     ra.tile_index = p.tile_index; ra.tile_count = p.tile_count; ra.rows_per_group = p.rows_per_group;
     ra.initstate = p.rng_initstate;
+    ra.isect_next = &cnt->isect_next;
 
     uint64_t iters = 0;
     for (uint32_t s0 = 0; s0 < p.spp; s0 += chunk) {

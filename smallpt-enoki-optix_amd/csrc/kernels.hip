@@ -17,11 +17,6 @@ struct TraceHit {
     float t, u, v;
 };
 
-// Stack-based BVH2 traversal, near child first, stack in LDS at
-// stk[i * kIsectBlock] (lane-interleaved: conflict-free, one bank per lane).
-// Closest hit: smallest t, ties broken toward the smaller original triangle
-// id so the answer does not depend on the tree.  anyhit: stop at the first
-// accepted triangle (OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
 struct NoStats {
     __device__ void node() {}
     __device__ void tri() {}
@@ -34,27 +29,48 @@ struct TravStats {
     __device__ void step() { steps++; }
 };
 
-template <typename Stats = NoStats>
-__device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
-                                          bool anyhit, uint32_t* __restrict__ stk, Stats& stats) {
+// Stack-based BVH2 traversal, near child first, stack in LDS at
+// stk[i * kIsectBlock] (lane-interleaved: conflict-free, one bank per lane).
+// Closest hit: smallest t, ties broken toward the smaller original triangle
+// id so the answer does not depend on the tree.  anyhit: stop at the first
+// accepted triangle (OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT).
+//
+// Resumable: step() advances one node or one leaf and returns true when the
+// ray is finished, so a persistent wave can swap finished lanes for new rays.
+struct Tracer {
+    WoopRay wr;
+    V3 o;
+    float ix, iy, iz, tmin;
+    int32_t node;
+    uint32_t sp;
+    bool anyhit;
     TraceHit h;
-    h.slot = -1;
-    h.id = 0xffffffffu;
-    h.t = tmax;
-    h.u = 0.0f;
-    h.v = 0.0f;
-    if (sc.empty) return h;
-    const WoopRay wr = woop_setup(o, d);
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
-    const float4* __restrict__ nodes = sc.nodes;
-    const float4* __restrict__ tris = sc.tris;
-    int32_t node = 0;
-    uint32_t sp = 0;
-    while (true) {
+
+    __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_) {
+        o = o_;
+        wr = woop_setup(o_, d);
+        ix = 1.0f / d.x; iy = 1.0f / d.y; iz = 1.0f / d.z;
+        tmin = tmin_;
+        anyhit = anyhit_;
+        node = sc.empty ? kDone : 0;
+        sp = 0;
+        h.slot = -1; h.id = 0xffffffffu; h.t = tmax_; h.u = 0.0f; h.v = 0.0f;
+    }
+    static constexpr int32_t kDone = (int32_t)0x7fffffff;
+
+    __device__ __forceinline__ bool pop(const uint32_t* __restrict__ stk) {
+        if (sp == 0) { node = kDone; return true; }
+        sp--;
+        node = (int32_t)stk[sp * kIsectBlock];
+        return false;
+    }
+
+    template <typename Stats>
+    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
         stats.step();
         if (node >= 0) {
             stats.node();
-            const float4* np = nodes + (size_t)node * 4;
+            const float4* np = sc.nodes + (size_t)node * 4;
             const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
             const float a0 = (n0.x - o.x) * ix, a1 = (n0.y - o.x) * ix;
             const float b0 = (n0.z - o.y) * iy, b1 = (n0.w - o.y) * iy;
@@ -74,72 +90,114 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
                 stk[sp * kIsectBlock] = (uint32_t)(swp ? ch0 : ch1);
                 sp++;
                 node = swp ? ch1 : ch0;
-            } else if (h0) {
-                node = ch0;
-            } else if (h1) {
-                node = ch1;
-            } else {
-                if (sp == 0) break;
-                sp--;
-                node = (int32_t)stk[sp * kIsectBlock];
+                return false;
             }
-        } else {
-            const uint32_t code = ~(uint32_t)node;
-            const uint32_t first = code >> 3, cnt = (code & 7u) + 1u;
-            for (uint32_t i = 0; i < cnt; i++) {
-                stats.tri();
-                const uint32_t s = first + i;
-                const float4 t0 = tris[(size_t)s * 3], t1 = tris[(size_t)s * 3 + 1], t2 = tris[(size_t)s * 3 + 2];
-                float t, u, v;
-                if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), tmin, h.t, t,
-                              u, v)) {
-                    const uint32_t id = f2u(t0.w);
-                    if (t < h.t || id < h.id) {
-                        h.t = t;
-                        h.id = id;
-                        h.slot = (int32_t)s;
-                        h.u = u;
-                        h.v = v;
-                    }
+            if (h0) { node = ch0; return false; }
+            if (h1) { node = ch1; return false; }
+            return pop(stk);
+        }
+        const uint32_t code = ~(uint32_t)node;
+        const uint32_t first = code >> 3, cnt = (code & 7u) + 1u;
+        for (uint32_t i = 0; i < cnt; i++) {
+            stats.tri();
+            const uint32_t s = first + i;
+            const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
+            float t, u, v;
+            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), tmin, h.t, t, u, v)) {
+                const uint32_t id = f2u(t0.w);
+                if (t < h.t || id < h.id) {
+                    h.t = t;
+                    h.id = id;
+                    h.slot = (int32_t)s;
+                    h.u = u;
+                    h.v = v;
                 }
             }
-            if (anyhit && h.slot >= 0) break;
-            if (sp == 0) break;
-            sp--;
-            node = (int32_t)stk[sp * kIsectBlock];
         }
+        if (anyhit && h.slot >= 0) { node = kDone; return true; }
+        return pop(stk);
     }
-    return h;
+};
+
+template <typename Stats = NoStats>
+__device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
+                                          bool anyhit, uint32_t* __restrict__ stk, Stats& stats) {
+    Tracer tr;
+    tr.init(sc, o, d, tmin, tmax, anyhit);
+    if (tr.node != Tracer::kDone)
+        while (!tr.step(sc, stk, stats)) {
+        }
+    return tr.h;
 }
 
-// Wavefront isect over the path queue: one lane per queued ray.  The last
-// cast of a path only needs a yes/no answer (a miss is the only thing that
-// contributes, main.cpp:407), so it runs as an any-hit query.
+// Persistent wavefront isect over the path queue.  The grid holds only as
+// many workgroups as fit on the chip; each wave keeps 64 rays in flight and,
+// whenever a quarter of its lanes have finished (or all have), refills them
+// from a wave-private pool of queue indices, itself refilled kIsectChunk at a
+// time from the launch-wide counter *a.next.  That removes the per-launch
+// tail of slow blocks and keeps lanes busy across ray boundaries.
+// The last cast of a path only needs a yes/no answer (a miss is the only thing
+// that contributes, main.cpp:407), so it runs as an any-hit query.
 template <bool kStats>
 __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
-    const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
+    uint32_t* stk = lds_stack + threadIdx.x;
     const uint32_t n = *a.count;
-    if (i >= n) return;
-    const V3 o = v3(a.q.ox[i], a.q.oy[i], a.q.oz[i]);
-    const V3 d = v3(a.q.dx[i], a.q.dy[i], a.q.dz[i]);
-    const uint32_t depth = a.q.meta[i] & ((1u << kMetaDepthBits) - 1u);
-    const bool anyhit = depth + 1 >= a.max_depth;
     typename std::conditional<kStats, TravStats, NoStats>::type st;
-    const TraceHit h = trace(a.sc, o, d, kRayTmin, kRayTmax, anyhit, lds_stack + threadIdx.x, st);
+    Tracer tr;
+    uint32_t ray = 0;
+    bool busy = false;
+    uint32_t pool = 0, pool_end = 0;  // wave-uniform
+    bool drained = false;             // wave-uniform: the launch counter is exhausted
+    uint32_t wave_steps = 0;
+    while (true) {
+        uint64_t idle = __ballot(!busy);
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        if (nidle >= kRefillIdle || nidle == 64u) {
+            while (idle && !drained) {
+                if (pool == pool_end) {
+                    uint32_t base = 0;
+                    if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, kIsectChunk);
+                    base = (uint32_t)__shfl((int)base, 0);
+                    if (base >= n) { drained = true; break; }
+                    pool = base;
+                    pool_end = min(base + kIsectChunk, n);
+                }
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
+                if (!busy && rank < take) {
+                    ray = pool + rank;
+                    const V3 o = v3(a.q.ox[ray], a.q.oy[ray], a.q.oz[ray]);
+                    const V3 d = v3(a.q.dx[ray], a.q.dy[ray], a.q.dz[ray]);
+                    const uint32_t depth = a.q.meta[ray] & ((1u << kMetaDepthBits) - 1u);
+                    tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth);
+                    busy = true;
+                    if (tr.node == Tracer::kDone) {  // empty scene
+                        a.hit_slot[ray] = -1;
+                        busy = false;
+                    }
+                }
+                pool += take;
+                idle = __ballot(!busy);
+            }
+        }
+        if (!__ballot(busy)) break;
+        wave_steps++;
+        if (busy && tr.step(a.sc, stk, st)) {
+            a.hit_slot[ray] = tr.h.slot;
+            a.hit_t[ray] = tr.h.t;
+            a.hit_u[ray] = tr.h.u;
+            a.hit_v[ray] = tr.h.v;
+            busy = false;
+        }
+    }
     if constexpr (kStats) {
-        uint32_t wmax = st.steps;
-        for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off));
         atomicAdd(&a.trav_stats[0], (unsigned long long)st.nodes);
         atomicAdd(&a.trav_stats[1], (unsigned long long)st.tris);
         atomicAdd(&a.trav_stats[2], (unsigned long long)st.steps);
-        if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
-            atomicAdd(&a.trav_stats[3], (unsigned long long)wmax);
+        if ((threadIdx.x & 63u) == 0) atomicAdd(&a.trav_stats[3], (unsigned long long)wave_steps);
     }
-    a.hit_slot[i] = h.slot;
-    a.hit_t[i] = h.t;
-    a.hit_u[i] = h.u;
-    a.hit_v[i] = h.v;
 }
 
 // __raygen__rg (wavefront_isect.cu:80-112) semantics for the public C ABI.
@@ -199,6 +257,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     if (i == 0) {
         *a.cursor_out = cur + total;
         *a.qn_out = surv + total;
+        *a.isect_next = 0;
         if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
     }
     if (i >= total) return;
@@ -396,20 +455,41 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
 // ------------------------------------------------------------- launchers
 static inline uint32_t blocks_for(uint32_t items, uint32_t block) { return (items + block - 1) / block; }
 
-hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+// Workgroups resident on the whole chip for this LDS stack size (cached).
+template <bool kStats>
+static uint32_t persistent_blocks(size_t lds) {
+    static thread_local size_t cached_lds = 0;
+    static thread_local uint32_t cached = 0;
+    static thread_local int cached_dev = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (cached && cached_lds == lds && cached_dev == dev) return cached;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<kStats>, kIsectBlock, lds) !=
+            hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cached = (uint32_t)(per_cu * cus);
+    cached_lds = lds;
+    cached_dev = dev;
+    return cached;
+}
+
+template <bool kStats>
+static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
     const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
-    hipLaunchKernelGGL(isect_queue_kernel<false>, dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock), lds,
-                       s, a);
+    const uint32_t blocks = min(persistent_blocks<kStats>(lds), blocks_for(grid_items, kIsectBlock));
+    hipLaunchKernelGGL(isect_queue_kernel<kStats>, dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
 
+hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+    return launch_isect_queue_t<false>(a, grid_items, s);
+}
+
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
-    if (grid_items == 0) return hipSuccess;
-    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
-    hipLaunchKernelGGL(isect_queue_kernel<true>, dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock), lds,
-                       s, a);
-    return hipGetLastError();
+    return launch_isect_queue_t<true>(a, grid_items, s);
 }
 
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {

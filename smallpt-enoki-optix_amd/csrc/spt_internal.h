@@ -12,6 +12,8 @@ constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 constexpr uint32_t kShadeBlock = 256;       // shade: 4 waves, one queue atomic per block
 constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
+constexpr uint32_t kIsectChunk = 256;       // queue indices a wave takes per atomic
+constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
 
 // Path queue, structure of arrays (ray.h layout for the ray planes).
 struct PathQueue {
@@ -42,6 +44,7 @@ struct IsectQueueArgs {
     int32_t* hit_slot;
     float *hit_t, *hit_u, *hit_v;
     uint32_t max_depth;
+    uint32_t* next;                  // launch-wide ray counter (zeroed before the launch)
     unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
 };
 
@@ -79,6 +82,7 @@ struct RefillArgs {
     const uint64_t* cursor_in;
     uint64_t* cursor_out;       // written by thread 0 only
     uint32_t* qn_out;           // queue count for the next isect, thread 0 only
+    uint32_t* isect_next;       // zeroed by thread 0 for the next isect launch
     const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
     unsigned long long* stats;
     uint64_t work_end;          // W_total (work items of this chunk end here)

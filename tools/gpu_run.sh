@@ -32,6 +32,10 @@ for s in "$@"; do
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
+    listctr) run listctr 300 rocprofv3 -L ;;
+    pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex isect_queue -d gpurun_out/pmc_sq -o run --output-format csv -- python tools/trav_stats.py --depths 8 --spp 8 ;;
+    pmctcc) run pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --kernel-include-regex isect_queue -d gpurun_out/pmc_tcc -o run --output-format csv -- python tools/trav_stats.py --depths 8 --spp 8 ;;
+    pmctcp) run pmctcp 600 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TA_BUSY_avr TA_TA_BUSY_sum --kernel-include-regex isect_queue -d gpurun_out/pmc_tcp -o run --output-format csv -- python tools/trav_stats.py --depths 8 --spp 8 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
