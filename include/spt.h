@@ -116,6 +116,8 @@ typedef struct spt_scene_stats {
     uint64_t ntri, nodes, leaves;
     uint32_t max_depth;         /* BVH depth (sets the LDS stack depth) */
     uint32_t max_leaf;
+    uint32_t bvh_width;         /* 8: compressed 8-wide BVH (default), 2: BVH2 (env SPT_BVH=2) */
+    uint32_t reserved;
     uint64_t device_bytes;
     double build_ms;            /* host SAH build */
     double sah_cost;

@@ -1,0 +1,212 @@
+// bvh8_build.cpp — collapse the binned-SAH BVH2 (leaves <= 3 triangles) into
+// the compressed 8-wide layout of bvh_build.h (after Ylitie, Karras, Laine,
+// "Efficient Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs",
+// HPG 2017): greedy collapse (open the largest-area inner child until 8
+// children), octant-ordered child slots, 8-bit conservative quantisation.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "bvh_build.h"
+
+namespace spt {
+namespace {
+
+struct Kid {
+    float lo[3], hi[3];
+    int32_t code;  // BVH2 child code: >= 0 inner node, < 0 leaf ~(first << 3 | count - 1)
+    float area() const {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct Collapser {
+    const std::vector<float>& n2;          // BVH2 nodes, 16 floats each
+    const std::vector<uint32_t>& slot2tri;  // BVH2 leaf order -> triangle id
+    std::vector<uint32_t> nodes;           // BVH8 nodes, 20 words each
+    std::vector<uint32_t> tri_order;       // BVH8 triangle slot -> triangle id
+    uint32_t depth = 0;
+    uint64_t leaves = 0;
+
+    Kid child(int32_t node, int c) const {
+        const float* nd = &n2[(size_t)node * 16];
+        Kid k;
+        if (c == 0) {
+            k.lo[0] = nd[0]; k.hi[0] = nd[1]; k.lo[1] = nd[2]; k.hi[1] = nd[3]; k.lo[2] = nd[8]; k.hi[2] = nd[9];
+        } else {
+            k.lo[0] = nd[4]; k.hi[0] = nd[5]; k.lo[1] = nd[6]; k.hi[1] = nd[7]; k.lo[2] = nd[10]; k.hi[2] = nd[11];
+        }
+        std::memcpy(&k.code, &nd[12 + c], 4);
+        return k;
+    }
+
+    static uint32_t alloc(std::vector<uint32_t>& v, uint32_t count) {
+        uint32_t first = (uint32_t)(v.size() / 20);
+        v.resize(v.size() + (size_t)20 * count, 0u);
+        return first;
+    }
+
+    // Fill node `idx` from the kids list (the BVH2 children of one BVH2 node).
+    void emit(uint32_t idx, std::vector<Kid> kids, uint32_t level) {
+        depth = std::max(depth, level);
+        // Greedy collapse: open the largest-area inner kid while room remains.
+        while (kids.size() < 8) {
+            int best = -1;
+            float best_area = -1.0f;
+            for (size_t i = 0; i < kids.size(); i++)
+                if (kids[i].code >= 0 && kids[i].area() > best_area) {
+                    best_area = kids[i].area();
+                    best = (int)i;
+                }
+            if (best < 0) break;
+            int32_t c = kids[best].code;
+            kids[best] = child(c, 0);
+            kids.push_back(child(c, 1));
+        }
+        // Node box and octant-ordered slots: slot s gets the kid that rays of
+        // octant s (bit i set <=> direction component i negative) reach first.
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (const Kid& k : kids)
+            for (int a = 0; a < 3; a++) {
+                lo[a] = std::fmin(lo[a], k.lo[a]);
+                hi[a] = std::fmax(hi[a], k.hi[a]);
+            }
+        double ctr[3];
+        for (int a = 0; a < 3; a++) ctr[a] = 0.5 * ((double)lo[a] + (double)hi[a]);
+        int slot_of[8];
+        int kid_in[8];
+        for (int s = 0; s < 8; s++) kid_in[s] = -1;
+        {
+            double cost[8][8];
+            for (size_t k = 0; k < kids.size(); k++)
+                for (int s = 0; s < 8; s++) {
+                    double c = 0.0;
+                    for (int a = 0; a < 3; a++) {
+                        double d = 0.5 * ((double)kids[k].lo[a] + (double)kids[k].hi[a]) - ctr[a];
+                        c += ((s >> a) & 1) ? -d : d;
+                    }
+                    cost[k][s] = c;
+                }
+            bool kdone[8] = {false};
+            for (size_t n = 0; n < kids.size(); n++) {
+                double bc = INFINITY;
+                int bk = -1, bs = -1;
+                for (size_t k = 0; k < kids.size(); k++) {
+                    if (kdone[k]) continue;
+                    for (int s = 0; s < 8; s++)
+                        if (kid_in[s] < 0 && cost[k][s] < bc) { bc = cost[k][s]; bk = (int)k; bs = s; }
+                }
+                if (bk < 0) {  // NaN costs: first free slot
+                    for (size_t k = 0; k < kids.size(); k++)
+                        if (!kdone[k]) { bk = (int)k; break; }
+                    for (int s = 0; s < 8; s++)
+                        if (kid_in[s] < 0) { bs = s; break; }
+                }
+                kdone[bk] = true;
+                kid_in[bs] = bk;
+                slot_of[bk] = bs;
+            }
+        }
+        (void)slot_of;
+        // Quantisation frame: p = node lo, per-axis power-of-two step with
+        // 255 steps covering the node; child boxes rounded outward.
+        uint32_t* w = &nodes[(size_t)idx * 20];
+        int ebias[3];
+        for (int a = 0; a < 3; a++) {
+            double ext = (double)hi[a] - (double)lo[a];
+            int e = -100;
+            if (ext > 0.0) {
+                e = (int)std::ceil(std::log2(ext / 255.0));
+                while (std::ldexp(255.0, e) < ext) e++;
+                e = std::max(e, -100);
+            }
+            ebias[a] = e + 127;
+            std::memcpy(&w[a], &lo[a], 4);
+        }
+        uint32_t imask = 0;
+        uint8_t meta[8] = {0};
+        uint8_t qlo[3][8], qhi[3][8];
+        for (int s = 0; s < 8; s++)
+            for (int a = 0; a < 3; a++) { qlo[a][s] = 255; qhi[a][s] = 0; }  // empty: inverted
+        // triangles of the leaf kids, contiguous in slot order
+        const uint32_t tri_base = (uint32_t)tri_order.size();
+        uint32_t toff = 0;
+        uint32_t ninner = 0;
+        for (int s = 0; s < 8; s++) {
+            int k = kid_in[s];
+            if (k < 0) continue;
+            const Kid& kd = kids[k];
+            for (int a = 0; a < 3; a++) {
+                double step = std::ldexp(1.0, ebias[a] - 127);
+                double ql = std::floor(((double)kd.lo[a] - (double)lo[a]) / step);
+                double qh = std::ceil(((double)kd.hi[a] - (double)lo[a]) / step);
+                if (!(ql >= 0.0)) ql = 0.0;  // NaN-safe
+                if (!(qh <= 255.0)) qh = 255.0;
+                if (ql > 255.0) ql = 255.0;
+                if (qh < 0.0) qh = 0.0;
+                qlo[a][s] = (uint8_t)ql;
+                qhi[a][s] = (uint8_t)qh;
+            }
+            if (kd.code >= 0) {
+                imask |= 1u << s;
+                meta[s] = (uint8_t)(0x20u | (24u + (uint32_t)s));
+                ninner++;
+            } else {
+                const uint32_t code = ~(uint32_t)kd.code;
+                const uint32_t first = code >> 3, cnt = (code & 7u) + 1u;  // cnt <= 3 (max_leaf)
+                meta[s] = (uint8_t)((((1u << cnt) - 1u) << 5) | toff);
+                for (uint32_t i = 0; i < cnt; i++) tri_order.push_back(slot2tri[first + i]);
+                toff += cnt;
+                leaves++;
+            }
+        }
+        const uint32_t child_base = ninner ? alloc(nodes, ninner) : 0u;
+        w = &nodes[(size_t)idx * 20];  // (alloc may have moved the vector)
+        w[3] = (uint32_t)ebias[0] | ((uint32_t)ebias[1] << 8) | ((uint32_t)ebias[2] << 16) | (imask << 24);
+        w[4] = child_base;
+        w[5] = tri_base;
+        std::memcpy(&w[6], meta, 8);
+        for (int a = 0; a < 3; a++) {
+            std::memcpy(&w[8 + 2 * a], qlo[a], 8);
+            std::memcpy(&w[14 + 2 * a], qhi[a], 8);
+        }
+        // recurse into the inner kids, in slot order, at their reserved indices
+        uint32_t r = 0;
+        for (int s = 0; s < 8; s++) {
+            int k = kid_in[s];
+            if (k < 0 || kids[k].code < 0) continue;
+            const int32_t c = kids[k].code;
+            emit(child_base + r, {child(c, 0), child(c, 1)}, level + 1);
+            r++;
+        }
+    }
+};
+
+}  // namespace
+
+Bvh8BuildResult build_bvh8(const float* tv, uint64_t ntri) {
+    Bvh8BuildResult res;
+    if (ntri == 0) return res;
+    BvhBuildResult b2 = build_bvh(tv, ntri, 3);
+    Collapser col{b2.nodes, b2.slot2tri, {}, {}, 0, 0};
+    col.nodes.reserve(b2.nodes.size() / 16 * 20 / 4 + 20);
+    col.tri_order.reserve(ntri);
+    Collapser::alloc(col.nodes, 1);
+    // build_bvh duplicates a root leaf into both children: keep one copy.
+    int32_t c0, c1;
+    std::memcpy(&c0, &b2.nodes[12], 4);
+    std::memcpy(&c1, &b2.nodes[13], 4);
+    if (b2.nodes.size() == 16 && c0 < 0 && c0 == c1)
+        col.emit(0, {col.child(0, 0)}, 1);
+    else
+        col.emit(0, {col.child(0, 0), col.child(0, 1)}, 1);
+    res.nodes = std::move(col.nodes);
+    res.slot2tri = std::move(col.tri_order);
+    res.depth = col.depth;
+    res.leaves = col.leaves;
+    res.sah_cost = b2.sah_cost;
+    return res;
+}
+
+}  // namespace spt

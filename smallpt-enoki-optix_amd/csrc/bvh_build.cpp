@@ -56,6 +56,7 @@ int32_t leaf_code(uint64_t first, uint64_t count) {
 struct Builder {
     PrimRef* refs;
     double root_area_inv;
+    uint32_t max_leaf;
 
     // Returns the child code of range [b, e) and its box; inner nodes are
     // appended to st.nodes in depth-first order (parent before children).
@@ -124,7 +125,7 @@ struct Builder {
                 float parent_area = box.area();
                 float split_cost = kNodeCost + (parent_area > 0.0f ? best_cost / parent_area : 0.0f) * kTriCost;
                 float leaf_cost = (float)n * kTriCost;
-                if (n <= kMaxLeafSize && leaf_cost <= split_cost) return make_leaf();
+                if (n <= max_leaf && leaf_cost <= split_cost) return make_leaf();
                 int axis = best_axis;
                 float scale = (float)kBins * (1.0f - 1e-6f) / ext[axis];
                 float lo = cbox.lo[axis];
@@ -138,8 +139,8 @@ struct Builder {
             }
         }
         if (!split_found) {
-            if (n <= kMaxLeafSize && depth >= kSahDepthLimit) return make_leaf();
-            if (n <= kMaxLeafSize && best_axis < 0) return make_leaf();
+            if (n <= max_leaf && depth >= kSahDepthLimit) return make_leaf();
+            if (n <= max_leaf && best_axis < 0) return make_leaf();
             // object median on the widest centroid axis (bounded depth)
             int axis = 0;
             if (ext[1] > ext[axis]) axis = 1;
@@ -198,7 +199,7 @@ struct Builder {
 
 }  // namespace
 
-BvhBuildResult build_bvh(const float* tv, uint64_t ntri) {
+BvhBuildResult build_bvh(const float* tv, uint64_t ntri, uint32_t max_leaf) {
     BvhBuildResult res;
     if (ntri == 0) return res;
     std::vector<PrimRef> refs(ntri);
@@ -220,6 +221,7 @@ BvhBuildResult build_bvh(const float* tv, uint64_t ntri) {
     }
     Builder bld;
     bld.refs = refs.data();
+    bld.max_leaf = std::max<uint32_t>(1, std::min<uint32_t>(max_leaf, kMaxLeafSize));
     double ra = root.area();
     bld.root_area_inv = ra > 0.0 ? 1.0 / ra : 0.0;
     SubTree st;

@@ -27,6 +27,25 @@ struct BvhBuildResult {
 };
 
 // tri_verts: ntri x 9 floats (v0 v1 v2).  ntri == 0 gives an empty result.
-BvhBuildResult build_bvh(const float* tri_verts, uint64_t ntri);
+// Leaves hold at most max_leaf (<= kMaxLeafSize) triangles.
+BvhBuildResult build_bvh(const float* tri_verts, uint64_t ntri, uint32_t max_leaf = kMaxLeafSize);
+
+// Compressed 8-wide BVH (80 B per node = 20 words, see kernels.hip Tracer8):
+//   w0-2  p.xyz        quantisation origin (f32)
+//   w3    ex | ey<<8 | ez<<16 | imask<<24   (biased exponents; imask: inner slots)
+//   w4    child_base   first inner child (inner children are contiguous, slot order)
+//   w5    tri_base     first triangle slot of this node's leaves (contiguous)
+//   w6-7  meta[8]      0 empty; inner 0b001_(24+s); leaf unary(count)<<5 | offset
+//   w8-9  qlo.x[8]  w10-11 qlo.y[8]  w12-13 qlo.z[8]
+//   w14-15 qhi.x[8] w16-17 qhi.y[8]  w18-19 qhi.z[8]
+// Child slots are ordered by ray octant (slot s is nearest for octant s).
+struct Bvh8BuildResult {
+    std::vector<uint32_t> nodes;     // 20 words per node
+    std::vector<uint32_t> slot2tri;  // triangle slot -> original triangle id
+    uint32_t depth = 0;              // deepest node level (root = 1)
+    uint64_t leaves = 0;
+    double sah_cost = 0.0;           // of the underlying BVH2
+};
+Bvh8BuildResult build_bvh8(const float* tri_verts, uint64_t ntri);
 
 }  // namespace spt

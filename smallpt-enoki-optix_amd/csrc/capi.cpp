@@ -8,6 +8,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -107,6 +108,7 @@ struct spt_scene_t {
     int device = 0;
     uint64_t ntri = 0;
     float4* nodes = nullptr;
+    uint4* nodes8 = nullptr;
     float4* tris = nullptr;
     float4* snrm = nullptr;
     float* tc = nullptr;
@@ -119,13 +121,13 @@ struct spt_scene_t {
 
     DeviceScene dev() const {
         DeviceScene d;
-        d.nodes = nodes; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
+        d.nodes = nodes; d.nodes8 = nodes8; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
         d.albedo = albedo; d.nmat = nmat; d.stack_depth = stack_depth; d.empty = ntri == 0;
         return d;
     }
     void release() {
         ws.release();
-        hfree(nodes); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
+        hfree(nodes); hfree(nodes8); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
     }
 };
 
@@ -292,7 +294,17 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
                                 (unsigned long long)t, (long long)ti);
             }
     }
-    BvhBuildResult bvh = build_bvh(tv.data(), ntri);
+    // Acceleration structure: the compressed 8-wide BVH by default; SPT_BVH=2
+    // selects the plain BVH2 (kept as the simple reference layout).
+    const char* kind = std::getenv("SPT_BVH");
+    const bool use8 = !(kind && std::strcmp(kind, "2") == 0);
+    BvhBuildResult bvh;
+    Bvh8BuildResult bvh8;
+    if (use8)
+        bvh8 = build_bvh8(tv.data(), ntri);
+    else
+        bvh = build_bvh(tv.data(), ntri);
+    const std::vector<uint32_t>& slot2tri = use8 ? bvh8.slot2tri : bvh.slot2tri;
     const double t1 = now_ms();
 
     // Slot-ordered device arrays.
@@ -300,7 +312,7 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
     std::vector<float> h_tc(tc_tri && tc ? (size_t)ntri * 6 : 0);
     std::vector<int32_t> h_o2s((size_t)ntri);
     for (uint64_t s = 0; s < ntri; s++) {
-        const uint32_t t = bvh.slot2tri[s];
+        const uint32_t t = slot2tri[s];
         h_o2s[t] = (int32_t)s;
         const float* v = &tv[(size_t)t * 9];
         for (int k = 0; k < 3; k++) {
@@ -329,10 +341,14 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
     spt_scene_t* sc = new spt_scene_t();
     (void)hipGetDevice(&sc->device);
     sc->ntri = ntri;
-    sc->stack_depth = std::max<uint32_t>(1, bvh.max_depth + 1);
+    sc->stack_depth = std::max<uint32_t>(1, (use8 ? bvh8.depth : bvh.max_depth) + 1);
     const float one[3] = {1.0f, 1.0f, 1.0f};
     spt_status us = SPT_OK;
-    if (!us) us = upload(&sc->nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+    if (use8) {
+        if (!us) us = upload(&sc->nodes8, bvh8.nodes.data(), bvh8.nodes.size() * sizeof(uint32_t));
+    } else {
+        if (!us) us = upload(&sc->nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+    }
     if (!us) us = upload(&sc->tris, h_tris.data(), h_tris.size() * sizeof(float4));
     if (!us) us = upload(&sc->snrm, h_snrm.data(), h_snrm.size() * sizeof(float4));
     if (!us) us = upload(&sc->tc, h_tc.data(), h_tc.size() * sizeof(float));
@@ -346,13 +362,15 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
     sc->nmat = 1;
     spt_scene_stats& ss = sc->stats;
     ss.ntri = ntri;
-    ss.nodes = bvh.nodes.size() / 16;
-    ss.leaves = bvh.leaves;
-    ss.max_depth = bvh.max_depth;
-    ss.max_leaf = bvh.max_leaf;
-    ss.device_bytes = bvh.nodes.size() * 4 + (h_tris.size() + h_snrm.size()) * 16 + h_tc.size() * 4 + h_o2s.size() * 4;
+    ss.nodes = use8 ? bvh8.nodes.size() / 20 : bvh.nodes.size() / 16;
+    ss.leaves = use8 ? bvh8.leaves : bvh.leaves;
+    ss.max_depth = use8 ? bvh8.depth : bvh.max_depth;
+    ss.max_leaf = use8 ? 3 : bvh.max_leaf;
+    ss.bvh_width = use8 ? 8 : 2;
+    ss.device_bytes = (use8 ? bvh8.nodes.size() : bvh.nodes.size()) * 4 + (h_tris.size() + h_snrm.size()) * 16 +
+                      h_tc.size() * 4 + h_o2s.size() * 4;
     ss.build_ms = t1 - t0;
-    ss.sah_cost = bvh.sah_cost;
+    ss.sah_cost = use8 ? bvh8.sah_cost : bvh.sah_cost;
     *out = sc;
     return SPT_OK;
 }

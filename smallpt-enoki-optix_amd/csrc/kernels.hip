@@ -57,6 +57,8 @@ struct Tracer {
         h.slot = -1; h.id = 0xffffffffu; h.t = tmax_; h.u = 0.0f; h.v = 0.0f;
     }
     static constexpr int32_t kDone = (int32_t)0x7fffffff;
+    static constexpr uint32_t kStackWords = 1;
+    __device__ __forceinline__ bool finished() const { return node == kDone; }
 
     __device__ __forceinline__ bool pop(const uint32_t* __restrict__ stk) {
         if (sp == 0) { node = kDone; return true; }
@@ -119,12 +121,147 @@ struct Tracer {
     }
 };
 
-template <typename Stats = NoStats>
+// Compressed 8-wide BVH traversal (layout: bvh_build.h; after Ylitie et al.
+// 2017).  A "node group" (nbase, nhits) holds the unvisited inner children of
+// one node: hit bits 24..31 at position 24 + (slot ^ oct_inv), so the highest
+// bit is the child nearest for this ray's octant, and the node's inner-slot
+// mask in bits 0..7 (child index = nbase + popc(imask below slot)).  A
+// "triangle group" (tbase, thits) holds the triangles of the hit leaves.
+// Child slabs are evaluated as t = q * (2^e / d) + (p - o) / d with one fma;
+// each axis is widened by a margin that bounds the fp32 error of that form
+// relative to the exact quantised planes (which already enclose the child),
+// so culling stays conservative and the closest hit is the exact Woop one.
+constexpr float kMarginRel = 1e-6f;
+constexpr float kMinDir = 1e-20f;
+
+struct Tracer8 {
+    WoopRay wr;
+    V3 o;
+    float ix, iy, iz, tmin;
+    uint32_t oct_inv;
+    uint32_t nbase, nhits, tbase, thits;
+    uint32_t sp;
+    bool anyhit, done;
+    TraceHit h;
+    static constexpr uint32_t kStackWords = 2;
+    __device__ __forceinline__ bool finished() const { return done; }
+
+    __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_) {
+        o = o_;
+        wr = woop_setup(o_, d);
+        const float dx = fabsf(d.x) < kMinDir ? copysignf(kMinDir, d.x) : d.x;
+        const float dy = fabsf(d.y) < kMinDir ? copysignf(kMinDir, d.y) : d.y;
+        const float dz = fabsf(d.z) < kMinDir ? copysignf(kMinDir, d.z) : d.z;
+        ix = 1.0f / dx; iy = 1.0f / dy; iz = 1.0f / dz;
+        const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
+        oct_inv = oct ^ 7u;
+        tmin = tmin_;
+        anyhit = anyhit_;
+        nbase = 0;
+        nhits = (1u << (24u + oct_inv)) | 1u;  // the root as slot 0 of a virtual parent
+        tbase = 0;
+        thits = 0;
+        sp = 0;
+        done = sc.empty != 0;
+        h.slot = -1; h.id = 0xffffffffu; h.t = tmax_; h.u = 0.0f; h.v = 0.0f;
+    }
+
+    __device__ __forceinline__ void visit(const DeviceScene& sc, uint32_t node) {
+        const uint4* np = sc.nodes8 + (size_t)node * 5;
+        const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+        const uint32_t ew = w0.w;
+        const uint32_t imask = ew >> 24;
+        const float ax = u2f((ew & 0xffu) << 23) * ix;
+        const float ay = u2f(((ew >> 8) & 0xffu) << 23) * iy;
+        const float az = u2f(((ew >> 16) & 0xffu) << 23) * iz;
+        const float bx = (u2f(w0.x) - o.x) * ix;
+        const float by = (u2f(w0.y) - o.y) * iy;
+        const float bz = (u2f(w0.z) - o.z) * iz;
+        const float mx = (fabsf(bx) + 255.0f * fabsf(ax)) * kMarginRel;
+        const float my = (fabsf(by) + 255.0f * fabsf(ay)) * kMarginRel;
+        const float mz = (fabsf(bz) + 255.0f * fabsf(az)) * kMarginRel;
+        const float bxe = bx - mx, bxx = bx + mx, bye = by - my, byx = by + my, bze = bz - mz, bzx = bz + mz;
+        // entry planes are the lo planes for a positive direction, hi otherwise
+        const bool px = ix >= 0.0f, py = iy >= 0.0f, pz = iz >= 0.0f;
+        const uint32_t exl = px ? w2.x : w3.z, exh = px ? w2.y : w3.w, xxl = px ? w3.z : w2.x, xxh = px ? w3.w : w2.y;
+        const uint32_t eyl = py ? w2.z : w4.x, eyh = py ? w2.w : w4.y, xyl = py ? w4.x : w2.z, xyh = py ? w4.y : w2.w;
+        const uint32_t ezl = pz ? w3.x : w4.z, ezh = pz ? w3.y : w4.w, xzl = pz ? w4.z : w3.x, xzh = pz ? w4.w : w3.y;
+        uint32_t hm = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < 8; c++) {
+            const uint32_t sh = (c & 3u) * 8u;
+            const bool lo = c < 4;
+            const float tex = fmaf((float)(((lo ? exl : exh) >> sh) & 0xffu), ax, bxe);
+            const float txx = fmaf((float)(((lo ? xxl : xxh) >> sh) & 0xffu), ax, bxx);
+            const float tey = fmaf((float)(((lo ? eyl : eyh) >> sh) & 0xffu), ay, bye);
+            const float txy = fmaf((float)(((lo ? xyl : xyh) >> sh) & 0xffu), ay, byx);
+            const float tez = fmaf((float)(((lo ? ezl : ezh) >> sh) & 0xffu), az, bze);
+            const float txz = fmaf((float)(((lo ? xzl : xzh) >> sh) & 0xffu), az, bzx);
+            const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tmin));
+            const float tf = fminf(fminf(txx, txy), fminf(txz, h.t));
+            if (tn <= tf) {
+                const uint32_t m = ((lo ? w1.z : w1.w) >> sh) & 0xffu;
+                uint32_t shift = m & 31u;
+                if ((imask >> c) & 1u) shift ^= oct_inv;
+                hm |= (m >> 5) << shift;
+            }
+        }
+        nbase = w1.x;
+        tbase = w1.y;
+        nhits = (hm & 0xff000000u) | imask;
+        thits = hm & 0x00ffffffu;
+    }
+
+    template <typename Stats>
+    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+        stats.step();
+        if (thits) {
+            stats.tri();
+            const uint32_t s = tbase + (uint32_t)__builtin_ctz(thits);
+            thits &= thits - 1u;
+            const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
+            float t, u, v;
+            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), tmin, h.t, t, u, v)) {
+                const uint32_t id = f2u(t0.w);
+                if (t < h.t || id < h.id) {
+                    h.t = t;
+                    h.id = id;
+                    h.slot = (int32_t)s;
+                    h.u = u;
+                    h.v = v;
+                }
+                if (anyhit) { done = true; return true; }
+            }
+            return false;
+        }
+        if (nhits & 0xff000000u) {
+            stats.node();
+            const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
+            const uint32_t slot = (bit - 24u) ^ oct_inv;
+            const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
+            nhits &= ~(1u << bit);
+            if (nhits & 0xff000000u) {
+                stk[(2 * sp) * kIsectBlock] = nbase;
+                stk[(2 * sp + 1) * kIsectBlock] = nhits;
+                sp++;
+            }
+            visit(sc, child);
+            return false;
+        }
+        if (sp == 0) { done = true; return true; }
+        sp--;
+        nbase = stk[(2 * sp) * kIsectBlock];
+        nhits = stk[(2 * sp + 1) * kIsectBlock];
+        return false;
+    }
+};
+
+template <typename Tr, typename Stats = NoStats>
 __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
                                           bool anyhit, uint32_t* __restrict__ stk, Stats& stats) {
-    Tracer tr;
+    Tr tr;
     tr.init(sc, o, d, tmin, tmax, anyhit);
-    if (tr.node != Tracer::kDone)
+    if (!tr.finished())
         while (!tr.step(sc, stk, stats)) {
         }
     return tr.h;
@@ -138,13 +275,13 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
 // tail of slow blocks and keeps lanes busy across ray boundaries.
 // The last cast of a path only needs a yes/no answer (a miss is the only thing
 // that contributes, main.cpp:407), so it runs as an any-hit query.
-template <bool kStats>
+template <typename Tr, bool kStats>
 __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
     uint32_t* stk = lds_stack + threadIdx.x;
     const uint32_t n = *a.count;
     typename std::conditional<kStats, TravStats, NoStats>::type st;
-    Tracer tr;
+    Tr tr;
     uint32_t ray = 0;
     bool busy = false;
     uint32_t pool = 0, pool_end = 0;  // wave-uniform
@@ -173,7 +310,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
                     const uint32_t depth = a.q.meta[ray] & ((1u << kMetaDepthBits) - 1u);
                     tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth);
                     busy = true;
-                    if (tr.node == Tracer::kDone) {  // empty scene
+                    if (tr.finished()) {  // empty scene
                         a.hit_slot[ray] = -1;
                         busy = false;
                     }
@@ -211,7 +348,9 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     const V3 d = v3(a.dx[i], a.dy[i], a.dz[i]);
     const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
     NoStats st;
-    const TraceHit h = trace(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x, st);
+    const TraceHit h = a.sc.nodes8
+                           ? trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x, st)
+                           : trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x, st);
     if (h.slot < 0) {
         a.tri_id[i] = -1;
         return;
@@ -456,7 +595,7 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
 static inline uint32_t blocks_for(uint32_t items, uint32_t block) { return (items + block - 1) / block; }
 
 // Workgroups resident on the whole chip for this LDS stack size (cached).
-template <bool kStats>
+template <typename Tr, bool kStats>
 static uint32_t persistent_blocks(size_t lds) {
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
@@ -465,7 +604,7 @@ static uint32_t persistent_blocks(size_t lds) {
     (void)hipGetDevice(&dev);
     if (cached && cached_lds == lds && cached_dev == dev) return cached;
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<kStats>, kIsectBlock, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<Tr, kStats>, kIsectBlock, lds) !=
             hipSuccess || per_cu <= 0)
         per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
@@ -475,26 +614,28 @@ static uint32_t persistent_blocks(size_t lds) {
     return cached;
 }
 
-template <bool kStats>
+template <typename Tr, bool kStats>
 static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
-    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
-    const uint32_t blocks = min(persistent_blocks<kStats>(lds), blocks_for(grid_items, kIsectBlock));
-    hipLaunchKernelGGL(isect_queue_kernel<kStats>, dim3(blocks), dim3(kIsectBlock), lds, s, a);
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t);
+    const uint32_t blocks = min(persistent_blocks<Tr, kStats>(lds), blocks_for(grid_items, kIsectBlock));
+    hipLaunchKernelGGL((isect_queue_kernel<Tr, kStats>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
-    return launch_isect_queue_t<false>(a, grid_items, s);
+    return a.sc.nodes8 ? launch_isect_queue_t<Tracer8, false>(a, grid_items, s)
+                       : launch_isect_queue_t<Tracer, false>(a, grid_items, s);
 }
 
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
-    return launch_isect_queue_t<true>(a, grid_items, s);
+    return a.sc.nodes8 ? launch_isect_queue_t<Tracer8, true>(a, grid_items, s)
+                       : launch_isect_queue_t<Tracer, true>(a, grid_items, s);
 }
 
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);
+    const size_t lds = (size_t)a.sc.stack_depth * (a.sc.nodes8 ? 2u : 1u) * kIsectBlock * sizeof(uint32_t);
     hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }

@@ -26,14 +26,15 @@ struct PathQueue {
 
 // Geometry on device, leaf ("slot") order.
 struct DeviceScene {
-    const float4* nodes;   // 4 per node (bvh_build.h)
+    const float4* nodes;   // BVH2: 4 per node (bvh_build.h)
+    const uint4* nodes8;   // compressed BVH8: 5 per node (bvh_build.h); non-null selects it
     const float4* tris;    // 3 per slot: v0 (w = original id bits), v1, v2
     const float4* snrm;    // 3 per slot: n0 (w = material id bits), n1, n2
     const float* tc;       // 6 per slot (u0 v0 u1 v1 u2 v2) or null
     const int32_t* orig2slot;
     const float* albedo;   // 3 per material
     uint32_t nmat;
-    uint32_t stack_depth;  // LDS stack entries per lane
+    uint32_t stack_depth;  // LDS stack entries per lane (BVH8 entries are 2 words)
     uint32_t empty;        // no triangles
 };
 

@@ -80,7 +80,8 @@ class RenderStats(ctypes.Structure):
 
 class SceneStats(ctypes.Structure):
     _fields_ = [("ntri", c_uint64), ("nodes", c_uint64), ("leaves", c_uint64),
-                ("max_depth", c_uint32), ("max_leaf", c_uint32), ("device_bytes", c_uint64),
+                ("max_depth", c_uint32), ("max_leaf", c_uint32), ("bvh_width", c_uint32), ("reserved", c_uint32),
+                ("device_bytes", c_uint64),
                 ("build_ms", c_double), ("sah_cost", c_double)]
 
     def as_dict(self) -> dict:

@@ -26,6 +26,7 @@ for s in "$@"; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     tests) run tests 900 python -m pytest tests -m gpu -q -x ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
+    tests2) run tests2 900 env SPT_BVH=2 python -m pytest tests -m gpu -q -x ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
