@@ -269,10 +269,10 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
 
 // Persistent wavefront isect over the path queue.  The grid holds only as
 // many workgroups as fit on the chip; each wave keeps 64 rays in flight and,
-// whenever a quarter of its lanes have finished (or all have), refills them
-// from a wave-private pool of queue indices, itself refilled kIsectChunk at a
-// time from the launch-wide counter *a.next.  That removes the per-launch
-// tail of slow blocks and keeps lanes busy across ray boundaries.
+// whenever kRefillIdle lanes have finished (or all have), refills them from
+// its work pool.  Each wave first owns a static contiguous share of 3/4 of the
+// queue (no atomics), then takes kIsectChunk-ray chunks of the remaining
+// quarter from the launch-wide counter *a.next, which evens out the tail.
 // The last cast of a path only needs a yes/no answer (a miss is the only thing
 // that contributes, main.cpp:407), so it runs as an any-hit query.
 template <typename Tr, bool kStats>
@@ -284,18 +284,23 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
     Tr tr;
     uint32_t ray = 0;
     bool busy = false;
-    uint32_t pool = 0, pool_end = 0;  // wave-uniform
-    bool drained = false;             // wave-uniform: the launch counter is exhausted
+    // wave-uniform pool state
+    const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
+    const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t share = (uint32_t)(((uint64_t)n * 3 / 4) / nwaves);
+    const uint32_t dyn_base = share * nwaves;
+    uint32_t pool = wave_id * share, pool_end = pool + share;
+    bool drained = false;
     uint32_t wave_steps = 0;
     while (true) {
         uint64_t idle = __ballot(!busy);
         const uint32_t nidle = (uint32_t)__popcll(idle);
         if (nidle >= kRefillIdle || nidle == 64u) {
-            while (idle && !drained) {
+            while (idle && !(drained && pool == pool_end)) {
                 if (pool == pool_end) {
                     uint32_t base = 0;
                     if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, kIsectChunk);
-                    base = (uint32_t)__shfl((int)base, 0);
+                    base = dyn_base + (uint32_t)__shfl((int)base, 0);
                     if (base >= n) { drained = true; break; }
                     pool = base;
                     pool_end = min(base + kIsectChunk, n);

@@ -12,7 +12,7 @@ constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 constexpr uint32_t kShadeBlock = 1024;      // shade: 16 waves, one queue atomic per block
 constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
-constexpr uint32_t kIsectChunk = 256;       // queue indices a wave takes per atomic
+constexpr uint32_t kIsectChunk = 64;        // dynamic-share queue indices a wave takes per atomic
 constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
 
 // Path queue, structure of arrays (ray.h layout for the ray planes).
