@@ -88,7 +88,7 @@ typedef struct spt_render_params {
     /* Interleaved row-group tiling: global row r belongs to tile
      * (r / rows_per_group) % tile_count.  tile_count = 1 renders the image. */
     uint32_t tile_index, tile_count, rows_per_group;
-    uint32_t wavefront_paths;   /* paths in flight per launch (0 = auto, ~2M) */
+    uint32_t wavefront_paths;   /* paths in flight per launch (0 = auto: 8M) */
     uint32_t rr_start_depth;    /* Russian roulette from this cast on (>= max_depth: off) */
     uint32_t rng_order;         /* SPT_RNG_* */
     uint64_t rng_initstate;     /* PCG32_DEFAULT_STATE 0x853c49e6748fea9b (main.cpp:376) */

@@ -234,24 +234,25 @@ struct Tracer8 {
             }
             return false;
         }
-        if (nhits & 0xff000000u) {
-            stats.node();
-            const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
-            const uint32_t slot = (bit - 24u) ^ oct_inv;
-            const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
-            nhits &= ~(1u << bit);
-            if (nhits & 0xff000000u) {
-                stk[(2 * sp) * kIsectBlock] = nbase;
-                stk[(2 * sp + 1) * kIsectBlock] = nhits;
-                sp++;
-            }
-            visit(sc, child);
-            return false;
+        if (!(nhits & 0xff000000u)) {
+            // current group exhausted: pop the next one (stacked groups always
+            // hold inner children) and visit its nearest child in this step
+            if (sp == 0) { done = true; return true; }
+            sp--;
+            nbase = stk[(2 * sp) * kIsectBlock];
+            nhits = stk[(2 * sp + 1) * kIsectBlock];
         }
-        if (sp == 0) { done = true; return true; }
-        sp--;
-        nbase = stk[(2 * sp) * kIsectBlock];
-        nhits = stk[(2 * sp + 1) * kIsectBlock];
+        stats.node();
+        const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
+        const uint32_t slot = (bit - 24u) ^ oct_inv;
+        const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
+        nhits &= ~(1u << bit);
+        if (nhits & 0xff000000u) {
+            stk[(2 * sp) * kIsectBlock] = nbase;
+            stk[(2 * sp + 1) * kIsectBlock] = nhits;
+            sp++;
+        }
+        visit(sc, child);
         return false;
     }
 };
