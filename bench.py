@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "isect_traffic.json")  # tools/pmc_traffic.py output
 ISECT_BYTES_PER_CAST = 44      # ray 24 B + meta 4 B in, hit 16 B out
 
 
@@ -154,6 +155,10 @@ def main():
         avg_ms = agg["isect_ms"] / launches
         bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic, traffic_src = None, None
+        if os.path.exists(TRAFFIC_JSON):  # FETCH_SIZE/WRITE_SIZE passes of this command (profiles/)
+            tj = json.load(open(TRAFFIC_JSON))
+            traffic, traffic_src = round(tj["traffic_bytes_per_launch"]), tj["source"][0].rsplit("/", 1)[0]
         rec = {
             "metric": "Mpaths/sec (pixels x spp / s), mitsuba.obj-standin 1024^2 x 64spp, depth 8",
             "value": round(value, 3),
@@ -171,7 +176,8 @@ def main():
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
                        "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "isect_queue_kernel", "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
                          "grays_per_s": round(agg["ray_casts"] / (agg["isect_ms"] * 1e-3) / 1e9, 4)
