@@ -11,7 +11,7 @@ for ctrs in "$@"; do
   i=$((i+1))
   echo "== pass $i: $ctrs"
   timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-include-regex isect_queue -d "$out/p$i" -o run --output-format csv \
-      -- python tools/trav_stats.py --depths 8 --spp 8 > "$out/p$i.log" 2>&1
+      -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$out/p$i.log" 2>&1
   rc=$?
   echo "== pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$i.log"; fi
