@@ -47,6 +47,14 @@ void hfree(T*& p) {
     p = nullptr;
 }
 
+// Tuning knobs read from the environment (defaults are the measured best).
+uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return dflt;
+    long x = std::strtol(v, nullptr, 10);
+    return (uint32_t)std::max<long>(lo, std::min<long>(hi, x));
+}
+
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -531,6 +539,9 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
     ia.trav_stats = trav_stats ? cnt->trav : nullptr;
     ia.next = &cnt->isect_next;
+    ia.refill_idle = env_u32("SPT_REFILL_IDLE", kRefillIdle, 1, 64);
+    ia.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 192, 0, 255);
+    ia.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
     ShadeArgs sa;
     sa.sc = sc->dev();
     sa.hit_slot = hit_slot; sa.hit_t = hit_t; sa.hit_u = hit_u; sa.hit_v = hit_v;

@@ -288,7 +288,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
     // wave-uniform pool state
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
     const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
-    const uint32_t share = (uint32_t)(((uint64_t)n * 3 / 4) / nwaves);
+    const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
     const uint32_t dyn_base = share * nwaves;
     uint32_t pool = wave_id * share, pool_end = pool + share;
     bool drained = false;
@@ -296,15 +296,15 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
     while (true) {
         uint64_t idle = __ballot(!busy);
         const uint32_t nidle = (uint32_t)__popcll(idle);
-        if (nidle >= kRefillIdle || nidle == 64u) {
+        if (nidle >= a.refill_idle) {
             while (idle && !(drained && pool == pool_end)) {
                 if (pool == pool_end) {
                     uint32_t base = 0;
-                    if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, kIsectChunk);
+                    if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, a.chunk);
                     base = dyn_base + (uint32_t)__shfl((int)base, 0);
                     if (base >= n) { drained = true; break; }
                     pool = base;
-                    pool_end = min(base + kIsectChunk, n);
+                    pool_end = min(base + a.chunk, n);
                 }
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));

@@ -46,6 +46,9 @@ struct IsectQueueArgs {
     float *hit_t, *hit_u, *hit_v;
     uint32_t max_depth;
     uint32_t* next;                  // launch-wide ray counter (zeroed before the launch)
+    uint32_t refill_idle;            // refill a wave once this many lanes are idle (1..64)
+    uint32_t static_share_q8;        // static share of the queue per wave, in 1/256ths
+    uint32_t chunk;                  // dynamic chunk (rays per atomic)
     unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
 };
 
