@@ -127,7 +127,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
-           "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0}
+           "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0}
     st = {}
     for _ in range(args.steps):
         st = step()
@@ -151,7 +151,7 @@ def main():
     value = paths / elapsed / 1e6
     if rank == 0:
         # isect roofline: algorithmic bytes per launch / average launch time (rank 0's tile)
-        launches = max(agg["iterations"], 1)
+        launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
         bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0

@@ -101,7 +101,7 @@ typedef struct spt_render_stats {
     uint64_t ray_casts;         /* closest/any-hit queries traced */
     uint64_t continuations;     /* paths that bounced into a next cast */
     uint64_t regenerations;     /* camera rays started by refills after the first launch */
-    uint64_t iterations;        /* isect+shade launch pairs */
+    uint64_t iterations;        /* isect+shade+refill rounds (each over every sub-wavefront) */
     uint32_t paths_in_flight;   /* wavefront capacity (queue slots) */
     uint32_t tile_rows;
     double isect_ms, shade_ms, camera_ms, resolve_ms; /* SPT_FLAG_TIMING only (camera = refills) */
@@ -110,6 +110,9 @@ typedef struct spt_render_stats {
     uint64_t isect_tris;        /*   triangle tests */
     uint64_t isect_lane_steps;  /*   traversal loop iterations summed over lanes */
     uint64_t isect_wave_steps;  /*   traversal loop iterations summed over waves */
+    uint64_t isect_launches;    /* SPT_FLAG_TIMING: isect launches timed (all streams) */
+    uint32_t streams;           /* sub-wavefronts (HIP streams) used, env SPT_STREAMS */
+    uint32_t reserved;
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

@@ -75,37 +75,61 @@ PathQueue carve_queue(char* base, size_t cap) {
     return q;
 }
 
-// Device counters of one render (zeroed per call; see spt_render).
+// Device counters of one sub-wavefront (zeroed per chunk; see spt_render).
 struct Counters {
     uint32_t qn[2];      // queue counts (isect/shade input)
     uint32_t surv[2];    // survivors appended by shade
     uint64_t cursor[2];  // next work item (double-buffered across refills)
-    unsigned long long stats[3];  // casts, continuations, camera rays started
-    unsigned long long trav[4];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps
-    uint32_t isect_next;          // persistent isect work counter (zeroed by each refill)
-    uint32_t pad;
+    uint32_t isect_next; // persistent isect work counter (zeroed by each refill)
+    uint32_t pad[3];
 };
 
-struct Workspace {
-    size_t cap = 0, film_cap = 0, jump_cap = 0;
+// Render-wide device statistics.
+struct Stats {
+    unsigned long long stats[3];  // casts, continuations, camera rays started
+    unsigned long long trav[4];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps
+    unsigned long long pad;
+};
+
+constexpr int kMaxStreams = 4;
+
+// One sub-wavefront: its own double-buffered path queue, hit records and
+// counters, driven on its own stream so its launch tails overlap the others'.
+struct Sub {
+    size_t cap = 0;
     char* qa = nullptr;
     char* qb = nullptr;
     char* hits = nullptr;
+    Counters* cnt = nullptr;
+    hipStream_t stream = nullptr;       // internal stream (sub 0 runs on the caller's)
+    uint32_t* host_counts = nullptr;    // pinned, 2 slots
+    hipEvent_t count_ev[2] = {nullptr, nullptr};
+    hipEvent_t join_ev = nullptr;
+};
+
+struct Workspace {
+    Sub sub[kMaxStreams];
+    size_t film_cap = 0, jump_cap = 0;
     float* film = nullptr;
     PcgJump* jumps = nullptr;
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
-    Counters* counters = nullptr;
-    uint32_t* host_counts = nullptr;        // pinned, 2 slots
-    uint64_t* host_cursor = nullptr;        // pinned, 2 slots
+    Stats* stats = nullptr;
+    uint64_t* host_cursor = nullptr;    // pinned, kMaxStreams slots
+    hipEvent_t fork_ev = nullptr;
     std::vector<hipEvent_t> events;
-    hipEvent_t count_ev[2] = {nullptr, nullptr};
 
     void release() {
-        hfree(qa); hfree(qb); hfree(hits); hfree(film); hfree(counters); hfree(jumps);
-        if (host_counts) (void)hipHostFree(host_counts);
+        for (Sub& b : sub) {
+            hfree(b.qa); hfree(b.qb); hfree(b.hits); hfree(b.cnt);
+            if (b.host_counts) (void)hipHostFree(b.host_counts);
+            for (auto& e : b.count_ev) if (e) (void)hipEventDestroy(e);
+            if (b.join_ev) (void)hipEventDestroy(b.join_ev);
+            if (b.stream) (void)hipStreamDestroy(b.stream);
+        }
+        hfree(film); hfree(jumps); hfree(stats);
         if (host_cursor) (void)hipHostFree(host_cursor);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
         for (auto e : events) (void)hipEventDestroy(e);
-        for (auto& e : count_ev) if (e) (void)hipEventDestroy(e);
         *this = Workspace();
     }
 };
@@ -180,14 +204,23 @@ Camera make_camera(const spt_render_params& p) {
     return cam;
 }
 
-spt_status ensure_workspace(Workspace& ws, size_t cap, size_t film_floats, size_t njumps) {
-    if (cap > ws.cap) {
-        hfree(ws.qa); hfree(ws.qb); hfree(ws.hits);
-        ws.cap = 0;
-        HIP_TRY(hipMalloc((void**)&ws.qa, kPathBytes * cap));
-        HIP_TRY(hipMalloc((void**)&ws.qb, kPathBytes * cap));
-        HIP_TRY(hipMalloc((void**)&ws.hits, kHitBytes * cap));
-        ws.cap = cap;
+spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, size_t film_floats, size_t njumps) {
+    for (int k = 0; k < nsub; k++) {
+        Sub& b = ws.sub[k];
+        if (cap > b.cap) {
+            hfree(b.qa); hfree(b.qb); hfree(b.hits);
+            b.cap = 0;
+            HIP_TRY(hipMalloc((void**)&b.qa, kPathBytes * cap));
+            HIP_TRY(hipMalloc((void**)&b.qb, kPathBytes * cap));
+            HIP_TRY(hipMalloc((void**)&b.hits, kHitBytes * cap));
+            b.cap = cap;
+        }
+        if (!b.cnt) HIP_TRY(hipMalloc((void**)&b.cnt, sizeof(Counters)));
+        if (!b.host_counts) HIP_TRY(hipHostMalloc((void**)&b.host_counts, 16, hipHostMallocDefault));
+        for (auto& e : b.count_ev)
+            if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        if (!b.join_ev) HIP_TRY(hipEventCreateWithFlags(&b.join_ev, hipEventDisableTiming));
+        if (k > 0 && !b.stream) HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
     }
     if (film_floats > ws.film_cap) {
         hfree(ws.film);
@@ -202,11 +235,10 @@ spt_status ensure_workspace(Workspace& ws, size_t cap, size_t film_floats, size_
         HIP_TRY(hipMalloc((void**)&ws.jumps, sizeof(PcgJump) * njumps));
         ws.jump_cap = njumps;
     }
-    if (!ws.counters) HIP_TRY(hipMalloc((void**)&ws.counters, sizeof(Counters)));
-    if (!ws.host_counts) HIP_TRY(hipHostMalloc((void**)&ws.host_counts, 16, hipHostMallocDefault));
-    if (!ws.host_cursor) HIP_TRY(hipHostMalloc((void**)&ws.host_cursor, 16, hipHostMallocDefault));
-    for (auto& e : ws.count_ev)
-        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!ws.stats) HIP_TRY(hipMalloc((void**)&ws.stats, sizeof(Stats)));
+    if (!ws.host_cursor) HIP_TRY(hipHostMalloc((void**)&ws.host_cursor, sizeof(uint64_t) * kMaxStreams,
+                                              hipHostMallocDefault));
+    if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
     return SPT_OK;
 }
 
@@ -484,14 +516,20 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);
+    // The wavefront is split into K sub-wavefronts on their own streams, so one
+    // sub-wavefront's launch tail overlaps the others' work.
+    int K = (int)env_u32("SPT_STREAMS", 2, 1, kMaxStreams);
+    if ((uint64_t)K > C) K = (int)C;
+    const uint64_t Ck = (C + K - 1) / K;
     // Per-sample contribution film [chunk][3][P], at most ~4 GiB per chunk.
     const uint64_t budget = 4ull << 30;
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(p.spp, budget / (12 * P)));
     rs.paths_in_flight = (uint32_t)C;
-    spt_status st = ensure_workspace(sc->ws, C, (size_t)chunk * 3 * P + 3 * P, p.spp);
+    spt_status st = ensure_workspace(sc->ws, K, Ck, (size_t)chunk * 3 * P + 3 * P, p.spp);
     if (st) return st;
     Workspace& ws = sc->ws;
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
+    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
 
     // PCG32 jump to each sample's first draw: s * (4 + 2D) (main.cpp:395,396,413).
     const uint64_t per_sample = 4ull + 2ull * p.max_depth;
@@ -504,132 +542,173 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     }
 
     const Camera cam = make_camera(p);
-    PathQueue q[2] = {carve_queue(ws.qa, ws.cap), carve_queue(ws.qb, ws.cap)};
-    int32_t* hit_slot = (int32_t*)ws.hits;
-    float* hit_t = (float*)(hit_slot + ws.cap);
-    float* hit_u = hit_t + ws.cap;
-    float* hit_v = hit_u + ws.cap;
     float* sfilm = ws.film;
     float* acc = ws.film + (size_t)chunk * 3 * P;
-    Counters* cnt = ws.counters;
+    hipStream_t strm[kMaxStreams];
+    for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
+    HIP_TRY(hipMemsetAsync(ws.stats, 0, sizeof(Stats), stream));
 
-    HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(Counters), stream));
     std::vector<std::pair<size_t, int>> timed;  // (start event index, 0 refill 1 isect 2 shade 3 resolve)
     size_t ev = 0;
-    auto mark = [&](int kind, auto&& launch) -> spt_status {
+    auto mark = [&](int kind, hipStream_t sk, auto&& launch) -> spt_status {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         spt_status s2;
         if (timing) {
             if ((s2 = get_event(ws, ev, &e0)) || (s2 = get_event(ws, ev + 1, &e1))) return s2;
-            HIP_TRY(hipEventRecord(e0, stream));
+            HIP_TRY(hipEventRecord(e0, sk));
         }
         HIP_TRY(launch());
         if (timing) {
-            HIP_TRY(hipEventRecord(e1, stream));
+            HIP_TRY(hipEventRecord(e1, sk));
             timed.push_back({ev, kind});
             ev += 2;
         }
         return SPT_OK;
     };
 
-    IsectQueueArgs ia;
-    ia.sc = sc->dev();
-    ia.hit_slot = hit_slot; ia.hit_t = hit_t; ia.hit_u = hit_u; ia.hit_v = hit_v;
-    ia.max_depth = p.max_depth;
-    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
-    ia.trav_stats = trav_stats ? cnt->trav : nullptr;
-    ia.next = &cnt->isect_next;
-    ia.refill_idle = env_u32("SPT_REFILL_IDLE", kRefillIdle, 1, 64);
-    ia.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 192, 0, 255);
-    ia.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
-    ShadeArgs sa;
-    sa.sc = sc->dev();
-    sa.hit_slot = hit_slot; sa.hit_t = hit_t; sa.hit_u = hit_u; sa.hit_v = hit_v;
-    sa.sfilm = sfilm;
-    sa.stats = cnt->stats;
-    sa.P = (uint32_t)P; sa.W = p.width; sa.max_depth = p.max_depth;
-    sa.rr_start = p.rr_start_depth; sa.rng_order = p.rng_order;
-    sa.tile_index = p.tile_index; sa.tile_count = p.tile_count; sa.rows_per_group = p.rows_per_group;
-    sa.env_r = p.env[0]; sa.env_g = p.env[1]; sa.env_b = p.env[2];
-    RefillArgs ra;
-    ra.cam = cam;
-    ra.sample_jump = ws.jumps;
-    ra.stats = cnt->stats;
-    ra.capacity = (uint32_t)C; ra.P = (uint32_t)P; ra.W = p.width; ra.rng_order = p.rng_order;
-    ra.tile_index = p.tile_index; ra.tile_count = p.tile_count; ra.rows_per_group = p.rows_per_group;
-    ra.initstate = p.rng_initstate;
-    ra.isect_next = &cnt->isect_next;
+    // Per sub-wavefront kernel arguments (queues and counters differ).
+    IsectQueueArgs ia[kMaxStreams];
+    ShadeArgs sa[kMaxStreams];
+    RefillArgs ra[kMaxStreams];
+    PathQueue q[kMaxStreams][2];
+    for (int k = 0; k < K; k++) {
+        Sub& b = ws.sub[k];
+        q[k][0] = carve_queue(b.qa, b.cap);
+        q[k][1] = carve_queue(b.qb, b.cap);
+        IsectQueueArgs& I = ia[k];
+        I.sc = sc->dev();
+        I.hits = (float4*)b.hits;
+        I.max_depth = p.max_depth;
+        I.trav_stats = trav_stats ? ws.stats->trav : nullptr;
+        I.next = &b.cnt->isect_next;
+        I.refill_idle = env_u32("SPT_REFILL_IDLE", kRefillIdle, 1, 64);
+        I.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 160, 0, 255);
+        I.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
+        ShadeArgs& S = sa[k];
+        S.sc = sc->dev();
+        S.hits = (const float4*)b.hits;
+        S.sfilm = sfilm;
+        S.stats = ws.stats->stats;
+        S.P = (uint32_t)P; S.W = p.width; S.max_depth = p.max_depth;
+        S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
+        S.tile_index = p.tile_index; S.tile_count = p.tile_count; S.rows_per_group = p.rows_per_group;
+        S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];
+        RefillArgs& R = ra[k];
+        R.cam = cam;
+        R.sample_jump = ws.jumps;
+        R.stats = ws.stats->stats;
+        R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
+        R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
+        R.initstate = p.rng_initstate;
+        R.isect_next = &b.cnt->isect_next;
+    }
 
     uint64_t iters = 0;
     for (uint32_t s0 = 0; s0 < p.spp; s0 += chunk) {
         const uint32_t ns = std::min(chunk, p.spp - s0);
-        // Chunk start: empty queue 0, cursor at the chunk's first work item.
-        HIP_TRY(hipMemsetAsync(cnt, 0, offsetof(Counters, stats), stream));
-        const uint64_t w0 = (uint64_t)s0 * P;
-        // Pinned source, read when the copy executes: every earlier copy has
-        // completed (the previous chunk synchronised on later events).
-        ws.host_cursor[0] = w0;
-        HIP_TRY(hipMemcpyAsync(&cnt->cursor[1], ws.host_cursor, sizeof(uint64_t), hipMemcpyHostToDevice, stream));
-        ra.work_end = w0 + (uint64_t)ns * P;
-        sa.sample0 = s0;
-        // initial fill of queue 0 (survivors = 0 from the zeroed surv[0])
-        ra.q = q[0]; ra.surv = &cnt->surv[0]; ra.cursor_in = &cnt->cursor[1]; ra.cursor_out = &cnt->cursor[0];
-        ra.qn_out = &cnt->qn[0];
-        if ((st = mark(0, [&] { return launch_refill(ra, (uint32_t)C, stream); }))) return st;
-
-        // isect -> shade -> refill until the queue drains.  The live count is
-        // read back once per batch, one batch behind the launches; it never
-        // exceeds C, so a stale value is a safe grid size.
-        const uint64_t max_iters = ((uint64_t)ns * P * p.max_depth + C - 1) / C + p.max_depth + 64;
-        uint32_t known = (uint32_t)C;
+        const uint64_t w0 = (uint64_t)s0 * P, L = (uint64_t)ns * P;
+        // fork: the sub-wavefront streams start after everything queued so far
+        HIP_TRY(hipEventRecord(ws.fork_ev, stream));
+        for (int k = 1; k < K; k++) HIP_TRY(hipStreamWaitEvent(strm[k], ws.fork_ev, 0));
+        for (int k = 0; k < K; k++) {
+            Sub& b = ws.sub[k];
+            // contiguous share of the chunk's work items (sample-major)
+            const uint64_t wb = w0 + L * k / K, we = w0 + L * (k + 1) / K;
+            HIP_TRY(hipMemsetAsync(b.cnt, 0, sizeof(Counters), strm[k]));
+            // Pinned source, read when the copy executes: every earlier copy has
+            // completed (the previous chunk synchronised on later events).
+            ws.host_cursor[k] = wb;
+            HIP_TRY(hipMemcpyAsync(&b.cnt->cursor[1], &ws.host_cursor[k], sizeof(uint64_t), hipMemcpyHostToDevice,
+                                   strm[k]));
+            ra[k].work_end = we;
+            sa[k].sample0 = s0;
+            ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = &b.cnt->cursor[1];
+            ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];
+            if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], (uint32_t)b.cap, strm[k]); }))) return st;
+        }
+        // isect -> shade -> refill per sub-wavefront until every queue drains.
+        // Live counts are read back once per batch, one batch behind the
+        // launches; they never grow, so a stale value is a safe grid size.
+        const uint64_t max_iters = (L * p.max_depth + Ck - 1) / Ck + p.max_depth + 64;
+        uint32_t known[kMaxStreams];
+        int cur[kMaxStreams], pending[kMaxStreams];
+        bool live[kMaxStreams];
+        for (int k = 0; k < K; k++) {
+            known[k] = (uint32_t)ws.sub[k].cap;
+            cur[k] = 0;
+            pending[k] = -1;
+            live[k] = true;
+        }
         uint64_t it = 0;
-        int cur = 0, pending = -1;
         uint32_t batch = 4, nbatch = 0;
-        while (true) {
-            for (uint32_t b = 0; b < batch; b++) {
-                const int nx = 1 - cur;
-                ia.q = q[cur];
-                ia.count = &cnt->qn[cur];
-                if ((st = mark(1, [&] {
-                         return trav_stats ? launch_isect_queue_stats(ia, known, stream)
-                                           : launch_isect_queue(ia, known, stream);
-                     })))
-                    return st;
-                HIP_TRY(hipMemsetAsync(&cnt->surv[nx], 0, sizeof(uint32_t), stream));
-                sa.in = q[cur]; sa.out = q[nx];
-                sa.count_in = &cnt->qn[cur];
-                sa.count_out = &cnt->surv[nx];
-                if ((st = mark(2, [&] { return launch_shade(sa, known, stream); }))) return st;
-                ra.q = q[nx]; ra.surv = &cnt->surv[nx]; ra.cursor_in = &cnt->cursor[cur];
-                ra.cursor_out = &cnt->cursor[nx]; ra.qn_out = &cnt->qn[nx];
-                if ((st = mark(0, [&] { return launch_refill(ra, (uint32_t)C, stream); }))) return st;
-                cur = nx;
+        int nlive = K;
+        while (nlive > 0) {
+            for (uint32_t bi = 0; bi < batch; bi++) {
+                for (int k = 0; k < K; k++) {
+                    if (!live[k]) continue;
+                    Sub& b = ws.sub[k];
+                    const int c = cur[k], nx = 1 - c;
+                    ia[k].q = q[k][c];
+                    ia[k].count = &b.cnt->qn[c];
+                    if ((st = mark(1, strm[k], [&] {
+                             return trav_stats ? launch_isect_queue_stats(ia[k], known[k], strm[k])
+                                               : launch_isect_queue(ia[k], known[k], strm[k]);
+                         })))
+                        return st;
+                    HIP_TRY(hipMemsetAsync(&b.cnt->surv[nx], 0, sizeof(uint32_t), strm[k]));
+                    sa[k].in = q[k][c]; sa[k].out = q[k][nx];
+                    sa[k].count_in = &b.cnt->qn[c];
+                    sa[k].count_out = &b.cnt->surv[nx];
+                    if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], known[k], strm[k]); }))) return st;
+                    ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
+                    ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
+                    if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], (uint32_t)b.cap, strm[k]); })))
+                        return st;
+                    cur[k] = nx;
+                }
                 it++;
             }
             const int slot = (int)(nbatch++ & 1u);
-            HIP_TRY(hipMemcpyAsync(ws.host_counts + slot, &cnt->qn[cur], sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                   stream));
-            HIP_TRY(hipEventRecord(ws.count_ev[slot], stream));
-            if (pending >= 0) {
-                HIP_TRY(hipEventSynchronize(ws.count_ev[pending]));
-                known = ws.host_counts[pending];
-                if (known == 0) break;
+            for (int k = 0; k < K; k++) {
+                if (!live[k]) continue;
+                Sub& b = ws.sub[k];
+                HIP_TRY(hipMemcpyAsync(b.host_counts + slot, &b.cnt->qn[cur[k]], sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, strm[k]));
+                HIP_TRY(hipEventRecord(b.count_ev[slot], strm[k]));
             }
-            pending = slot;
+            for (int k = 0; k < K; k++) {
+                if (!live[k]) continue;
+                Sub& b = ws.sub[k];
+                if (pending[k] >= 0) {
+                    HIP_TRY(hipEventSynchronize(b.count_ev[pending[k]]));
+                    known[k] = b.host_counts[pending[k]];
+                    if (known[k] == 0) {
+                        live[k] = false;
+                        nlive--;
+                        continue;
+                    }
+                }
+                pending[k] = slot;
+            }
             if (it > max_iters)
                 return fail(SPT_ERR_HIP, "spt_render: queue did not drain after %llu iterations",
                             (unsigned long long)it);
             batch = std::min<uint32_t>(batch * 2, 16);
         }
         iters += it;
-        if ((st = mark(3, [&] {
+        // join the sub-wavefront streams back into the caller's stream
+        for (int k = 1; k < K; k++) {
+            HIP_TRY(hipEventRecord(ws.sub[k].join_ev, strm[k]));
+            HIP_TRY(hipStreamWaitEvent(stream, ws.sub[k].join_ev, 0));
+        }
+        if ((st = mark(3, stream, [&] {
                  return launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
                                        stream);
              })))
             return st;
     }
     unsigned long long hstats[7] = {0, 0, 0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(hstats, cnt->stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(hstats, ws.stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
     rs.continuations = hstats[1];
@@ -640,15 +719,18 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     rs.isect_lane_steps = hstats[5];
     rs.isect_wave_steps = hstats[6];
     if (timing) {
+        uint64_t nis = 0;
         for (auto& tk : timed) {
             float ms = 0.0f;
             HIP_TRY(hipEventElapsedTime(&ms, ws.events[tk.first], ws.events[tk.first + 1]));
             if (tk.second == 0) rs.camera_ms += ms;
-            else if (tk.second == 1) rs.isect_ms += ms;
+            else if (tk.second == 1) { rs.isect_ms += ms; nis++; }
             else if (tk.second == 2) rs.shade_ms += ms;
             else rs.resolve_ms += ms;
         }
+        rs.isect_launches = nis;
     }
+    rs.streams = (uint32_t)K;
     rs.total_ms = now_ms() - wall0;
     if (stats_out) *stats_out = rs;
     return SPT_OK;

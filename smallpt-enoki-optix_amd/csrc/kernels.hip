@@ -317,7 +317,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
                     tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth);
                     busy = true;
                     if (tr.finished()) {  // empty scene
-                        a.hit_slot[ray] = -1;
+                        a.hits[ray] = make_float4(u2f(0xffffffffu), 0.0f, 0.0f, 0.0f);
                         busy = false;
                     }
                 }
@@ -328,10 +328,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
         if (!__ballot(busy)) break;
         wave_steps++;
         if (busy && tr.step(a.sc, stk, st)) {
-            a.hit_slot[ray] = tr.h.slot;
-            a.hit_t[ray] = tr.h.t;
-            a.hit_u[ray] = tr.h.u;
-            a.hit_v[ray] = tr.h.v;
+            a.hits[ray] = make_float4(u2f((uint32_t)tr.h.slot), tr.h.t, tr.h.u, tr.h.v);
             busy = false;
         }
     }
@@ -445,7 +442,8 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         const uint32_t meta = a.in.meta[i];
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
-        const int32_t slot = a.hit_slot[i];
+        const float4 hit = a.hits[i];
+        const int32_t slot = (int32_t)f2u(hit.x);
         tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
         bool term = true;
         float cr = 0.0f, cg = 0.0f, cb = 0.0f;
@@ -463,7 +461,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             rng.inc = ((uint64_t)gpix << 1u) | 1u;
             const V3 o = v3(a.in.ox[i], a.in.oy[i], a.in.oz[i]);
             const V3 d = v3(a.in.dx[i], a.in.dy[i], a.in.dz[i]);
-            const float t = a.hit_t[i], u = a.hit_u[i], v = a.hit_v[i];
+            const float t = hit.y, u = hit.z, v = hit.w;
             float xi_x, xi_y;
             draw2(rng, a.rng_order, xi_x, xi_y);               // main.cpp:413
             const float4 m0 = a.sc.snrm[(size_t)slot * 3];

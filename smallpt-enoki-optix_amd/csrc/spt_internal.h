@@ -12,7 +12,7 @@ constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 constexpr uint32_t kShadeBlock = 1024;      // shade: 16 waves, one queue atomic per block
 constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
-constexpr uint32_t kIsectChunk = 64;        // dynamic-share queue indices a wave takes per atomic
+constexpr uint32_t kIsectChunk = 128;       // dynamic-share queue indices a wave takes per atomic
 constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
 
 // Path queue, structure of arrays (ray.h layout for the ray planes).
@@ -42,8 +42,7 @@ struct IsectQueueArgs {
     DeviceScene sc;
     PathQueue q;
     const uint32_t* count;
-    int32_t* hit_slot;
-    float *hit_t, *hit_u, *hit_v;
+    float4* hits;                    // AoS per queue slot: (slot bits, t, u, v)
     uint32_t max_depth;
     uint32_t* next;                  // launch-wide ray counter (zeroed before the launch)
     uint32_t refill_idle;            // refill a wave once this many lanes are idle (1..64)
@@ -66,8 +65,7 @@ struct IsectPublicArgs {
 struct ShadeArgs {
     DeviceScene sc;
     PathQueue in, out;
-    const int32_t* hit_slot;
-    const float *hit_t, *hit_u, *hit_v;
+    const float4* hits;
     const uint32_t* count_in;
     uint32_t* count_out;        // survivors appended here (zeroed before the launch)
     float* sfilm;               // [spp_chunk][3][P]: one contribution per (sample, pixel)

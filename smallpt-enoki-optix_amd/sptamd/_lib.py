@@ -72,7 +72,8 @@ class RenderStats(ctypes.Structure):
                 ("isect_ms", c_double), ("shade_ms", c_double), ("camera_ms", c_double),
                 ("resolve_ms", c_double), ("total_ms", c_double),
                 ("isect_nodes", c_uint64), ("isect_tris", c_uint64), ("isect_lane_steps", c_uint64),
-                ("isect_wave_steps", c_uint64)]
+                ("isect_wave_steps", c_uint64), ("isect_launches", c_uint64), ("streams", c_uint32),
+                ("reserved", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
