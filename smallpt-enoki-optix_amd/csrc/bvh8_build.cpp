@@ -5,6 +5,7 @@
 // children), octant-ordered child slots, 8-bit conservative quantisation.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "bvh_build.h"
@@ -15,6 +16,7 @@ namespace {
 struct Kid {
     float lo[3], hi[3];
     int32_t code;  // BVH2 child code: >= 0 inner node, < 0 leaf ~(first << 3 | count - 1)
+    uint32_t ntri = 0;  // triangles in the subtree
     float area() const {
         float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
         return 2.0f * (dx * dy + dy * dz + dz * dx);
@@ -28,6 +30,33 @@ struct Collapser {
     std::vector<uint32_t> tri_order;       // BVH8 triangle slot -> triangle id
     uint32_t depth = 0;
     uint64_t leaves = 0;
+    std::vector<uint32_t> ntri2;           // triangles under each BVH2 inner node
+    int mode = 1;                          // 0: BVH2 leaves as is; 1: leaf-size-1 BVH2, fill to 8
+
+    uint32_t count_tris(int32_t code) {
+        if (code < 0) return ((~(uint32_t)code) & 7u) + 1u;
+        const float* nd = &n2[(size_t)code * 16];
+        int32_t c0, c1;
+        std::memcpy(&c0, &nd[12], 4);
+        std::memcpy(&c1, &nd[13], 4);
+        return ntri2[code] = count_tris(c0) + count_tris(c1);
+    }
+    // Leaf candidate: a subtree small enough to become one BVH8 leaf (<= 3 triangles).
+    bool leafable(const Kid& k) const { return k.code < 0 || (mode >= 1 && k.ntri <= 3); }
+    // Triangles (BVH2 leaf-order slots) of a subtree, in order.
+    void gather(int32_t code, std::vector<uint32_t>& out) const {
+        if (code < 0) {
+            const uint32_t c = ~(uint32_t)code;
+            for (uint32_t i = 0; i < (c & 7u) + 1u; i++) out.push_back((c >> 3) + i);
+            return;
+        }
+        const float* nd = &n2[(size_t)code * 16];
+        int32_t c0, c1;
+        std::memcpy(&c0, &nd[12], 4);
+        std::memcpy(&c1, &nd[13], 4);
+        gather(c0, out);
+        gather(c1, out);
+    }
 
     Kid child(int32_t node, int c) const {
         const float* nd = &n2[(size_t)node * 16];
@@ -38,6 +67,7 @@ struct Collapser {
             k.lo[0] = nd[4]; k.hi[0] = nd[5]; k.lo[1] = nd[6]; k.hi[1] = nd[7]; k.lo[2] = nd[10]; k.hi[2] = nd[11];
         }
         std::memcpy(&k.code, &nd[12 + c], 4);
+        k.ntri = k.code < 0 ? ((~(uint32_t)k.code) & 7u) + 1u : ntri2[k.code];
         return k;
     }
 
@@ -50,15 +80,23 @@ struct Collapser {
     // Fill node `idx` from the kids list (the BVH2 children of one BVH2 node).
     void emit(uint32_t idx, std::vector<Kid> kids, uint32_t level) {
         depth = std::max(depth, level);
-        // Greedy collapse: open the largest-area inner kid while room remains.
+        // Greedy collapse: open the largest-area kid that cannot be a leaf while
+        // room remains; in mode 2 then keep splitting multi-triangle leaf
+        // candidates (largest first) to fill the 8 slots.
         while (kids.size() < 8) {
             int best = -1;
             float best_area = -1.0f;
             for (size_t i = 0; i < kids.size(); i++)
-                if (kids[i].code >= 0 && kids[i].area() > best_area) {
+                if (kids[i].code >= 0 && !leafable(kids[i]) && kids[i].area() > best_area) {
                     best_area = kids[i].area();
                     best = (int)i;
                 }
+            if (best < 0 && mode >= 2)
+                for (size_t i = 0; i < kids.size(); i++)
+                    if (kids[i].code >= 0 && kids[i].area() > best_area) {
+                        best_area = kids[i].area();
+                        best = (int)i;
+                    }
             if (best < 0) break;
             int32_t c = kids[best].code;
             kids[best] = child(c, 0);
@@ -148,15 +186,16 @@ struct Collapser {
                 qlo[a][s] = (uint8_t)ql;
                 qhi[a][s] = (uint8_t)qh;
             }
-            if (kd.code >= 0) {
+            if (!leafable(kd)) {
                 imask |= 1u << s;
                 meta[s] = (uint8_t)(0x20u | (24u + (uint32_t)s));
                 ninner++;
             } else {
-                const uint32_t code = ~(uint32_t)kd.code;
-                const uint32_t first = code >> 3, cnt = (code & 7u) + 1u;  // cnt <= 3 (max_leaf)
+                std::vector<uint32_t> ts;
+                gather(kd.code, ts);  // <= 3 triangles
+                const uint32_t cnt = (uint32_t)ts.size();
                 meta[s] = (uint8_t)((((1u << cnt) - 1u) << 5) | toff);
-                for (uint32_t i = 0; i < cnt; i++) tri_order.push_back(slot2tri[first + i]);
+                for (uint32_t t : ts) tri_order.push_back(slot2tri[t]);
                 toff += cnt;
                 leaves++;
             }
@@ -175,7 +214,7 @@ struct Collapser {
         uint32_t r = 0;
         for (int s = 0; s < 8; s++) {
             int k = kid_in[s];
-            if (k < 0 || kids[k].code < 0) continue;
+            if (k < 0 || leafable(kids[k])) continue;
             const int32_t c = kids[k].code;
             emit(child_base + r, {child(c, 0), child(c, 1)}, level + 1);
             r++;
@@ -188,8 +227,19 @@ struct Collapser {
 Bvh8BuildResult build_bvh8(const float* tv, uint64_t ntri) {
     Bvh8BuildResult res;
     if (ntri == 0) return res;
-    BvhBuildResult b2 = build_bvh(tv, ntri, 3);
+    const char* m = std::getenv("SPT_BVH8_MODE");
+    const int mode = m ? std::atoi(m) : 1;
+    BvhBuildResult b2 = build_bvh(tv, ntri, mode >= 1 ? 1 : 3);
     Collapser col{b2.nodes, b2.slot2tri, {}, {}, 0, 0};
+    col.mode = mode;
+    col.ntri2.assign(b2.nodes.size() / 16, 0);
+    {
+        int32_t r0, r1;
+        std::memcpy(&r0, &b2.nodes[12], 4);
+        std::memcpy(&r1, &b2.nodes[13], 4);
+        col.count_tris(r0);
+        if (r1 != r0) col.count_tris(r1);
+    }
     col.nodes.reserve(b2.nodes.size() / 16 * 20 / 4 + 20);
     col.tri_order.reserve(ntri);
     Collapser::alloc(col.nodes, 1);
