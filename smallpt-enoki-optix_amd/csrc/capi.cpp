@@ -385,7 +385,12 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
     const float one[3] = {1.0f, 1.0f, 1.0f};
     spt_status us = SPT_OK;
     if (use8) {
-        if (!us) us = upload(&sc->nodes8, bvh8.nodes.data(), bvh8.nodes.size() * sizeof(uint32_t));
+        // pad each 80-B node to its own 128-B cache line (kNode8Quads x 16 B)
+        const size_t nn = bvh8.nodes.size() / 20;
+        std::vector<uint32_t> padded(nn * kNode8Quads * 4, 0u);
+        for (size_t i = 0; i < nn; i++)
+            std::memcpy(&padded[i * kNode8Quads * 4], &bvh8.nodes[i * 20], 80);
+        if (!us) us = upload(&sc->nodes8, padded.data(), padded.size() * sizeof(uint32_t));
     } else {
         if (!us) us = upload(&sc->nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
     }
@@ -407,7 +412,8 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
     ss.max_depth = use8 ? bvh8.depth : bvh.max_depth;
     ss.max_leaf = use8 ? 3 : bvh.max_leaf;
     ss.bvh_width = use8 ? 8 : 2;
-    ss.device_bytes = (use8 ? bvh8.nodes.size() : bvh.nodes.size()) * 4 + (h_tris.size() + h_snrm.size()) * 16 +
+    ss.device_bytes = (use8 ? bvh8.nodes.size() / 20 * kNode8Quads * 16 : bvh.nodes.size() * 4) +
+                      (h_tris.size() + h_snrm.size()) * 16 +
                       h_tc.size() * 4 + h_o2s.size() * 4;
     ss.build_ms = t1 - t0;
     ss.sah_cost = use8 ? bvh8.sah_cost : bvh.sah_cost;

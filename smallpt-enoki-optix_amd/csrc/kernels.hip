@@ -167,7 +167,7 @@ struct Tracer8 {
     }
 
     __device__ __forceinline__ void visit(const DeviceScene& sc, uint32_t node) {
-        const uint4* np = sc.nodes8 + (size_t)node * 5;
+        const uint4* np = sc.nodes8 + (size_t)node * kNode8Quads;
         const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
         const uint32_t ew = w0.w;
         const uint32_t imask = ew >> 24;

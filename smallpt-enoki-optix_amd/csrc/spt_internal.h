@@ -9,6 +9,7 @@
 namespace spt {
 
 constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
+constexpr uint32_t kNode8Quads = 8;         // BVH8 node stride in 16-B units (80 B used, padded to one 128-B line)
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 constexpr uint32_t kShadeBlock = 1024;      // shade: 16 waves, one queue atomic per block
 constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
