@@ -622,7 +622,9 @@ template <typename Tr, bool kStats>
 static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
     const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t);
-    const uint32_t blocks = min(persistent_blocks<Tr, kStats>(lds), blocks_for(grid_items, kIsectBlock));
+    const uint32_t full = persistent_blocks<Tr, kStats>(lds);
+    const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)full * a.grid_q8) >> 8)) : full;
+    const uint32_t blocks = min(scaled, blocks_for(grid_items, kIsectBlock));
     hipLaunchKernelGGL((isect_queue_kernel<Tr, kStats>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }

@@ -49,6 +49,7 @@ struct IsectQueueArgs {
     uint32_t refill_idle;            // refill a wave once this many lanes are idle (1..64)
     uint32_t static_share_q8;        // static share of the queue per wave, in 1/256ths
     uint32_t chunk;                  // dynamic chunk (rays per atomic)
+    uint32_t grid_q8;                // persistent grid scale in 1/256ths of full occupancy (0 = full)
     unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
 };
 
