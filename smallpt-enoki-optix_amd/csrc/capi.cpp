@@ -590,7 +590,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         I.refill_idle = env_u32("SPT_REFILL_IDLE", kRefillIdle, 1, 64);
         I.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 160, 0, 255);
         I.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
-        I.grid_q8 = env_u32("SPT_ISECT_GRID_Q8", 0, 0, 4096);
+        // each stream's persistent grid covers 1/K of the chip (measured best)
+        I.grid_q8 = env_u32("SPT_ISECT_GRID_Q8", 256u / (uint32_t)K, 0, 4096);
         ShadeArgs& S = sa[k];
         S.sc = sc->dev();
         S.hits = (const float4*)b.hits;
