@@ -29,34 +29,67 @@ TRAFFIC_JSON = os.path.join(ROOT, "profiles", "isect_traffic.json")  # tools/pmc
 ISECT_BYTES_PER_CAST = 44      # ray 24 B + meta 4 B in, hit 16 B out
 
 
+# BASELINE.json configs (index = position in "configs"); 1 is the headline.
+CONFIGS = {
+    1: dict(scene="mitsuba_synth", width=1024, height=1024, spp=64, depth=8, smallpt=False),
+    2: dict(scene="cornell_spheres", width=1024, height=1024, spp=1024, depth=10, smallpt=True),
+    3: dict(scene="mitsuba_synth", width=4096, height=4096, spp=256, depth=8, smallpt=False),
+    4: dict(scene="city_synth", width=1920, height=1080, spp=64, depth=8, smallpt=False),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--width", type=int, default=1024)
-    ap.add_argument("--height", type=int, default=1024)
-    ap.add_argument("--spp", type=int, default=64)
-    ap.add_argument("--depth", type=int, default=8)
-    ap.add_argument("--scene", default="mitsuba_synth")
+    ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
+                    help="BASELINE.json configs[i]: 1 mitsuba 1024^2x64 (headline), 2 Cornell 1024^2x1024 "
+                         "(emitters, albedo, roulette), 3 mitsuba 4096^2x256, 4 10M-tri city 1920x1080x64")
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--depth", type=int, default=0)
+    ap.add_argument("--scene", default="")
     ap.add_argument("--rows-per-group", type=int, default=8)
     ap.add_argument("--wavefront", type=int, default=0, help="paths in flight per launch (0 = auto)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save", default="", help="write the rank-0 image (.npy) here")
-    return ap.parse_args()
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    for k in ("scene", "width", "height", "spp", "depth"):
+        if not getattr(args, k):
+            setattr(args, k, cfg[k])
+    args.smallpt = cfg["smallpt"]
+    return args
 
 
-def cpu_baseline(mesh, args, threads):
+def workload(args, scenes):
+    """(mesh dict or OBJ path, render kwargs, albedo, emission) for the config.
+    smallpt mode (config 2): Kd albedo, Ke emitters, black sky, roulette from
+    cast 5, smallpt's camera; otherwise the reference's semantics (albedo 1,
+    sky 1, main.cpp:383 camera)."""
+    if args.scene == "city_synth":  # 10M triangles: arrays, not a 600 MB OBJ
+        src = scenes.city_synth(10_000_000)
+    else:
+        src = scenes.scene_obj(args.scene)
+    if not args.smallpt:
+        return src, {}, None, None
+    kw = dict(camera=scenes.cornell_camera(), rr_start_depth=5, env=(0.0, 0.0, 0.0))
+    return src, kw, True, True
+
+
+def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     """Oracle (oracle/, a C restatement of main.cpp:354-446) on a bounded row
     sample of the same workload, on this host's cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
 
-    sc = O.OracleScene(mesh)
-    p = O.reference_params(args.width, args.height, args.spp, args.depth)
+    sc = O.OracleScene(mesh, albedo=albedo, emission=emission)
+    p = O.reference_params(args.width, args.height, args.spp, args.depth, **kw)
     stride = 64
     rows = np.arange(0, args.height, stride, dtype=np.int32)[:4]
     t0 = time.perf_counter()
@@ -96,19 +129,34 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     # scene: generated stand-in, loaded through the OBJ reader like main.cpp:365
-    obj = scenes.scene_obj(args.scene) if rank == 0 or world == 1 else None
+    # (rank 0 writes the cached OBJ first)
+    if rank == 0 or world == 1:
+        src, kw, alb, emi = workload(args, scenes)
     if world > 1:
         dist.barrier()
-        obj = scenes.scene_obj(args.scene)
+        if rank != 0:
+            src, kw, alb, emi = workload(args, scenes)
     scene = sptamd.Scene()
-    scene.add_triangle_mesh(obj)
+    if isinstance(src, str):
+        scene.add_triangle_mesh(src)
+    else:
+        scene.add_arrays(src)
+    t_commit = time.perf_counter()
     scene.commit(local)
+    t_commit = time.perf_counter() - t_commit
+    mesh = scene.mesh
+    if alb:
+        alb, emi = scenes.smallpt_materials(mesh)
+        scene.backend.set_albedo(alb)
+        scene.backend.set_emission(emi)
+    else:
+        alb = emi = None
     sstats = scene.backend.stats
 
     W, H = args.width, args.height
     R = args.rows_per_group
     params = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
-                                wavefront_paths=args.wavefront, timing=True)
+                                wavefront_paths=args.wavefront, timing=True, **kw)
     dev = torch.device("cuda", local)
     tg = TileGather(H, W, rank, world, R, dev)
     film = tg.tile_view()
@@ -160,7 +208,8 @@ def main():
             tj = json.load(open(TRAFFIC_JSON))
             traffic, traffic_src = round(tj["traffic_bytes_per_launch"]), tj["source"][0].rsplit("/", 1)[0]
         rec = {
-            "metric": "Mpaths/sec (pixels x spp / s), mitsuba.obj-standin 1024^2 x 64spp, depth 8",
+            "metric": "Mpaths/sec (pixels x spp / s), mitsuba.obj-standin 1024^2 x 64spp, depth 8"
+                      if args.config == 1 else f"Mpaths/sec (pixels x spp / s), BASELINE config {args.config}",
             "value": round(value, 3),
             "unit": "Mpaths/s",
             "n_gpus": world,
@@ -171,8 +220,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (mitsuba_synth stand-in generated in-run; reference asset absent)",
-            "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}",
+            "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
+            "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
+                                   + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
+                                      if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
                        "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -184,13 +235,13 @@ def main():
                          if agg["isect_ms"] else None},
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
                                    ("isect_ms", "shade_ms", "camera_ms", "resolve_ms")},
-            "bvh": {k: sstats[k] for k in ("nodes", "max_depth", "build_ms", "sah_cost")},
+            "bvh": dict({k: sstats[k] for k in ("nodes", "max_depth", "build_ms", "sah_cost", "device_bytes")},
+                        commit_s=round(t_commit, 3)),
         }
         if args.save:
             np.save(args.save, tg.image.cpu().numpy())
         if world == 1 and not args.no_cpu_baseline:
-            mesh = scenes.load_obj(obj)
-            rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads)
+            rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads, kw, alb, emi)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

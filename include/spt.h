@@ -135,6 +135,7 @@ typedef struct spt_mesh {
     int32_t* mat_id;            /* per triangle: obj material id + 1 (main.cpp:185) */
     float* kd;                  /* (nmat) x 3 diffuse colours, [0] = default (main.cpp:229-245) */
     uint32_t nmat;
+    float* ke;                  /* (nmat) x 3 emitted radiance (.mtl Ke), [0] = 0; not read by the reference */
 } spt_mesh;
 
 /* ---------------------------------------------------------------- device */
@@ -156,6 +157,12 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
 /* Per-material albedo (RGB, nmat x 3).  Default: 1 for every material, as in
  * the reference (main.cpp:234,244 — Kd is read and discarded). */
 spt_status spt_scene_set_albedo(spt_scene scene, const float* albedo_rgb, uint32_t nmat);
+
+/* Per-material emitted radiance (RGB, nmat x 3), added as throughput x Le at
+ * every surface hit (smallpt's obj.e; the reference has no emitters, SURVEY
+ * F6 / §8f row 3).  Default: none.  With emitters the last cast is a closest
+ * hit (it must know which surface it reached). */
+spt_status spt_scene_set_emission(spt_scene scene, const float* emission_rgb, uint32_t nmat);
 
 spt_status spt_scene_get_stats(spt_scene scene, spt_scene_stats* out);
 spt_status spt_scene_destroy(spt_scene scene);

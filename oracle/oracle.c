@@ -234,6 +234,8 @@ typedef struct {
     int32_t* mat;   /* ntri */
     float* albedo;  /* nmat * 3 */
     int32_t nmat;
+    float* emission; /* nemit * 3 or NULL */
+    int32_t nemit;
     int32_t use_bvh;
     onode* nodes;
     int64_t nnodes;
@@ -335,10 +337,21 @@ void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nver
     return s;
 }
 
+void oracle_scene_set_emission(void* scene, const float* emission, int32_t nmat) {
+    oscene* s = (oscene*)scene;
+    free(s->emission);
+    s->emission = NULL;
+    s->nemit = 0;
+    if (!emission || nmat <= 0) return;
+    s->emission = (float*)malloc(sizeof(float) * 3 * (size_t)nmat);
+    memcpy(s->emission, emission, sizeof(float) * 3 * (size_t)nmat);
+    s->nemit = nmat;
+}
+
 void oracle_scene_destroy(void* scene) {
     oscene* s = (oscene*)scene;
     if (!s) return;
-    free(s->v); free(s->n); free(s->mat); free(s->albedo); free(s->nodes); free(s->prims);
+    free(s->v); free(s->n); free(s->mat); free(s->albedo); free(s->emission); free(s->nodes); free(s->prims);
     free(s);
 }
 
@@ -549,6 +562,7 @@ static void render_pixel(void* c_, int64_t li) {
     long long casts = 0;
     for (int32_t smp = 0; smp < p->spp; smp++) {                  /* main.cpp:385 */
         float contrib[3] = {1.0f, 1.0f, 1.0f};                    /* main.cpp:391 */
+        float L[3] = {0.0f, 0.0f, 0.0f};  /* this sample's radiance, added to film once */
         int active = 1;                                           /* main.cpp:392 */
         float xi_x, xi_y;
         draw2(&rng, p->rng_order, &xi_x, &xi_y);                  /* main.cpp:395 */
@@ -565,7 +579,13 @@ static void render_pixel(void* c_, int64_t li) {
                 trace(s, &r, 0.001f, 1e20f, 1, &h);               /* ray.h:15-17 */
                 casts++;
                 if (h.id < 0) {                                   /* main.cpp:407 */
-                    for (int k = 0; k < 3; k++) film[k] = film[k] + contrib[k] * p->env[k];
+                    for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * p->env[k];
+                } else if (s->emission) {
+                    /* emitted radiance at every hit (smallpt's obj.e; the
+                     * reference has no emitters — SURVEY §8f row 3) */
+                    int32_t me = s->mat[h.id];
+                    if (me >= 0 && me < s->nemit)
+                        for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * s->emission[me * 3 + k];
                 }
             }
             active = active && (h.id >= 0);                       /* main.cpp:410 */
@@ -594,6 +614,9 @@ static void render_pixel(void* c_, int64_t li) {
                 }
             }
         }
+        /* Without emitters L is 0 or contrib * env: the same film sum as the
+         * reference's per-miss film += contrib (main.cpp:407). */
+        for (int k = 0; k < 3; k++) film[k] = film[k] + L[k];
     }
     int64_t npx = c->nrow_pixels;
     for (int k = 0; k < 3; k++) c->film[k * npx + li] = film[k] / (float)p->spp; /* main.cpp:429 */

@@ -36,6 +36,8 @@ void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nver
                           const int32_t* mat_id, const float* albedo, int32_t nmat,
                           int32_t use_bvh);
 void oracle_scene_destroy(void* scene);
+/* Per-material emission (nmat x 3), NULL/0 = none (see oracle_render). */
+void oracle_scene_set_emission(void* scene, const float* emission, int32_t nmat);
 
 /* wavefront_isect.cu:80-112 semantics: masked lanes untouched; miss -> id -1. */
 void oracle_intersect(void* scene, const float* ox, const float* oy, const float* oz,

@@ -38,6 +38,7 @@ def _load():
     lib.oracle_scene_create.restype = vp
     lib.oracle_scene_create.argtypes = [vp, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp, c_int32, c_int32]
     lib.oracle_scene_destroy.argtypes = [vp]
+    lib.oracle_scene_set_emission.argtypes = [vp, vp, c_int32]
     lib.oracle_intersect.argtypes = [vp] + [vp] * 8 + [vp, c_uint32] + [vp] * 4 + [c_int64, c_int32, c_int32]
     lib.oracle_render.restype = c_int32
     lib.oracle_render.argtypes = [vp, POINTER(OracleParams), vp, c_int32, vp, c_int32, POINTER(c_uint64)]
@@ -82,7 +83,7 @@ def reference_params(width=512, height=512, spp=100, max_depth=2, camera=None, r
 
 
 class OracleScene:
-    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None):
+    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None):
         self.pt = np.ascontiguousarray(mesh["pos_tri"], dtype=np.int32)
         self.pos = np.ascontiguousarray(mesh["pos"], dtype=np.float32)
         self.nt = None if mesh.get("nrm_tri") is None else np.ascontiguousarray(mesh["nrm_tri"], dtype=np.int32)
@@ -95,9 +96,13 @@ class OracleScene:
                                          _p(self.nrm), 0 if self.nrm is None else self.nrm.size // 3,
                                          _p(self.mat), _p(self.alb), 0 if self.alb is None else self.alb.shape[0],
                                          1 if use_bvh else 0)
+        emi = emission if emission is not None else mesh.get("emission")
+        self.emi = None if emi is None else np.ascontiguousarray(emi, dtype=np.float32).reshape(-1, 3)
+        if self.emi is not None:
+            lib.oracle_scene_set_emission(self.h, _p(self.emi), self.emi.shape[0])
 
     def __del__(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and lib is not None:  # (module teardown at exit)
             lib.oracle_scene_destroy(self.h)
             self.h = None
 

@@ -59,8 +59,8 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// 52 B per path: rng u64 | 6 ray f32 | pix u32 | meta u32 | 3 throughput f32
-constexpr size_t kPathBytes = 8 + 6 * 4 + 4 + 4 + 3 * 4;
+// 64 B per path: rng u64 | 6 ray f32 | pix u32 | meta u32 | 3 throughput f32 | 3 radiance f32
+constexpr size_t kPathBytes = 8 + 6 * 4 + 4 + 4 + 3 * 4 + 3 * 4;
 constexpr size_t kHitBytes = 16;
 
 PathQueue carve_queue(char* base, size_t cap) {
@@ -72,6 +72,7 @@ PathQueue carve_queue(char* base, size_t cap) {
     q.pix = (uint32_t*)(f + 6 * cap);
     q.meta = q.pix + cap;
     q.tr = (float*)(q.meta + cap); q.tg = q.tr + cap; q.tb = q.tg + cap;
+    q.lr = q.tb + cap; q.lg = q.lr + cap; q.lb = q.lg + cap;
     return q;
 }
 
@@ -147,6 +148,8 @@ struct spt_scene_t {
     int32_t* orig2slot = nullptr;
     float* albedo = nullptr;
     uint32_t nmat = 1;
+    float* emission = nullptr;
+    uint32_t nemit = 0;
     uint32_t stack_depth = 1;
     spt_scene_stats stats{};
     Workspace ws;
@@ -154,12 +157,12 @@ struct spt_scene_t {
     DeviceScene dev() const {
         DeviceScene d;
         d.nodes = nodes; d.nodes8 = nodes8; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
-        d.albedo = albedo; d.nmat = nmat; d.stack_depth = stack_depth; d.empty = ntri == 0;
+        d.albedo = albedo; d.nmat = nmat; d.emission = emission; d.nemit = nemit; d.stack_depth = stack_depth; d.empty = ntri == 0;
         return d;
     }
     void release() {
         ws.release();
-        hfree(nodes); hfree(nodes8); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
+        hfree(nodes); hfree(nodes8); hfree(emission); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
     }
 };
 
@@ -429,6 +432,22 @@ spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t 
     hfree(sc->albedo);
     sc->albedo = d;
     sc->nmat = nmat;
+    return SPT_OK;
+}
+
+spt_status spt_scene_set_emission(spt_scene sc, const float* emission_rgb, uint32_t nmat) {
+    if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_emission: NULL scene");
+    hfree(sc->emission);
+    sc->nemit = 0;
+    if (!emission_rgb || nmat == 0) return SPT_OK;  // no emitters
+    bool any = false;
+    for (uint32_t i = 0; i < 3 * nmat; i++) any |= emission_rgb[i] != 0.0f;
+    if (!any) return SPT_OK;
+    float* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, sizeof(float) * 3 * nmat));
+    HIP_TRY(hipMemcpy(d, emission_rgb, sizeof(float) * 3 * nmat, hipMemcpyHostToDevice));
+    sc->emission = d;
+    sc->nemit = nmat;
     return SPT_OK;
 }
 

@@ -48,7 +48,8 @@ bool parse_index(const char*& p, int nv, int nt, int nn, Idx& out) {
     return out.v >= 0;
 }
 
-void load_mtl(const std::string& path, std::map<std::string, int>& names, std::vector<float>& kd) {
+void load_mtl(const std::string& path, std::map<std::string, int>& names, std::vector<float>& kd,
+              std::vector<float>& ke) {
     FILE* f = std::fopen(path.c_str(), "r");
     if (!f) return;
     char line[4096];
@@ -64,10 +65,12 @@ void load_mtl(const std::string& path, std::map<std::string, int>& names, std::v
             cur = (int)(kd.size() / 3);
             names[name] = cur;
             kd.push_back(0.0f); kd.push_back(0.0f); kd.push_back(0.0f);
-        } else if (cur >= 0 && p[0] == 'K' && p[1] == 'd' && (p[2] == ' ' || p[2] == '\t')) {
+            ke.push_back(0.0f); ke.push_back(0.0f); ke.push_back(0.0f);
+        } else if (cur >= 0 && p[0] == 'K' && (p[1] == 'd' || p[1] == 'e') && (p[2] == ' ' || p[2] == '\t')) {
             float r = 0, g = 0, b = 0;
             std::sscanf(p + 2, "%f %f %f", &r, &g, &b);
-            kd[cur * 3] = r; kd[cur * 3 + 1] = g; kd[cur * 3 + 2] = b;
+            std::vector<float>& dst = p[1] == 'd' ? kd : ke;
+            dst[cur * 3] = r; dst[cur * 3 + 1] = g; dst[cur * 3 + 2] = b;
         }
     }
     std::fclose(f);
@@ -94,7 +97,7 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
     size_t slash = dir.find_last_of('/');
     dir = slash == std::string::npos ? std::string() : dir.substr(0, slash + 1);
 
-    std::vector<float> pos, nrm, tc, kd;
+    std::vector<float> pos, nrm, tc, kd, ke;
     std::vector<int32_t> pt, nt, tt, mat;
     std::map<std::string, int> names;
     int cur_mat = -1;
@@ -152,7 +155,7 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
             while (*p == ' ' || *p == '\t') p++;
             std::string name(p);
             while (!name.empty() && (name.back() == '\n' || name.back() == '\r' || name.back() == ' ')) name.pop_back();
-            load_mtl(dir + name, names, kd);
+            load_mtl(dir + name, names, kd, ke);
         }
     }
     std::free(line);
@@ -166,6 +169,8 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
     // Material table: [0] = default, then one entry per .mtl material (its Kd).
     std::vector<float> kd_all(3, 1.0f);
     kd_all.insert(kd_all.end(), kd.begin(), kd.end());
+    std::vector<float> ke_all(3, 0.0f);  // Ke (emission, not read by the reference)
+    ke_all.insert(ke_all.end(), ke.begin(), ke.end());
 
     out->ntri = mat.size();
     out->nvert = pos.size() / 3;
@@ -179,6 +184,7 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
     out->tc = dup(tc);
     out->mat_id = dup(mat);
     out->kd = dup(kd_all);
+    out->ke = dup(ke_all);
     out->nmat = (uint32_t)(kd_all.size() / 3);
     return SPT_OK;
 }
@@ -187,6 +193,7 @@ void spt_mesh_free(spt_mesh* m) {
     if (!m) return;
     std::free(m->pos_tri); std::free(m->pos); std::free(m->nrm_tri); std::free(m->nrm);
     std::free(m->tc_tri); std::free(m->tc); std::free(m->mat_id); std::free(m->kd);
+    std::free(m->ke);
     std::memset(m, 0, sizeof(*m));
 }
 

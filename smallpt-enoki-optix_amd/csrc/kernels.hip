@@ -314,7 +314,8 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
                     const V3 o = v3(a.q.ox[ray], a.q.oy[ray], a.q.oz[ray]);
                     const V3 d = v3(a.q.dx[ray], a.q.dy[ray], a.q.dz[ray]);
                     const uint32_t depth = a.q.meta[ray] & ((1u << kMetaDepthBits) - 1u);
-                    tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth);
+                    // any-hit for the last cast unless emitters need the surface
+                    tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !a.sc.emission);
                     busy = true;
                     if (tr.finished()) {  // empty scene
                         a.hits[ray] = make_float4(u2f(0xffffffffu), 0.0f, 0.0f, 0.0f);
@@ -375,13 +376,15 @@ __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32
 }
 
 __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix,
-                                           uint32_t meta, uint64_t rng, float tr, float tg, float tb) {
+                                           uint32_t meta, uint64_t rng, float tr, float tg, float tb, float lr,
+                                           float lg, float lb) {
     q.ox[j] = o.x; q.oy[j] = o.y; q.oz[j] = o.z;
     q.dx[j] = d.x; q.dy[j] = d.y; q.dz[j] = d.z;
     q.pix[j] = pix;
     q.meta[j] = meta;
     q.rng[j] = rng;
     q.tr[j] = tr; q.tg[j] = tg; q.tb[j] = tb;
+    q.lr[j] = lr; q.lg[j] = lg; q.lb[j] = lb;
 }
 
 // Refill: start work items [cursor, cursor + total) in queue slots
@@ -414,7 +417,8 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     rng.state = pcg_apply(a.sample_jump[s], rng.state, rng.inc);
     V3 o, d;
     camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
-    store_path(a.q, surv + i, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f);  // main.cpp:391
+    store_path(a.q, surv + i, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f,
+               0.0f);  // main.cpp:391
 }
 
 // ----------------------------------------------------------------- shade
@@ -436,7 +440,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
     uint32_t pix = 0, nmeta = 0;
     uint64_t nrng = 0;
-    float tr = 1.0f, tg = 1.0f, tb = 1.0f;
+    float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     if (i < n) {
         pix = a.in.pix[i];
         const uint32_t meta = a.in.meta[i];
@@ -445,14 +449,23 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         const float4 hit = a.hits[i];
         const int32_t slot = (int32_t)f2u(hit.x);
         tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
+        lr = a.in.lr[i]; lg = a.in.lg[i]; lb = a.in.lb[i];
         bool term = true;
-        float cr = 0.0f, cg = 0.0f, cb = 0.0f;
         if (slot < 0) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
-            cr = tr * a.env_r;
-            cg = tg * a.env_g;
-            cb = tb * a.env_b;
-        } else if (depth + 1 < a.max_depth) {
+            lr = lr + tr * a.env_r;
+            lg = lg + tg * a.env_g;
+            lb = lb + tb * a.env_b;
+        } else if (a.sc.emission) {
+            // emitted radiance at the hit (smallpt obj.e; not in the reference)
+            uint32_t mat = f2u(a.sc.snrm[(size_t)slot * 3].w);
+            if (mat < a.sc.nemit) {
+                lr = lr + tr * a.sc.emission[mat * 3];
+                lg = lg + tg * a.sc.emission[mat * 3 + 1];
+                lb = lb + tb * a.sc.emission[mat * 3 + 2];
+            }
+        }
+        if (slot >= 0 && depth + 1 < a.max_depth) {
             const uint32_t lx = pix % a.W, ly = pix / a.W;
             const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
             const uint32_t gpix = gy * a.W + lx;
@@ -501,9 +514,9 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         // else: hit on the last cast — the path ends without contribution.
         if (term) {
             float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
-            f[0] = cr;
-            f[(size_t)a.P] = cg;
-            f[(size_t)2 * a.P] = cb;
+            f[0] = lr;
+            f[(size_t)a.P] = lg;
+            f[(size_t)2 * a.P] = lb;
         }
     }
 
@@ -532,7 +545,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
     }
     __syncthreads();
-    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb);
+    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb, lr, lg, lb);
 }
 
 // Per-pixel sum of the per-sample contributions in sample order

@@ -23,6 +23,7 @@ struct PathQueue {
     uint32_t* meta;   // sample << 8 | cast index
     uint64_t* rng;    // PCG32 state (inc = 2 * global_pixel + 1)
     float *tr, *tg, *tb;  // path throughput
+    float *lr, *lg, *lb;  // radiance gathered so far (emission hits)
 };
 
 // Geometry on device, leaf ("slot") order.
@@ -35,6 +36,8 @@ struct DeviceScene {
     const int32_t* orig2slot;
     const float* albedo;   // 3 per material
     uint32_t nmat;
+    const float* emission; // 3 per material or null (no emitters)
+    uint32_t nemit;
     uint32_t stack_depth;  // LDS stack entries per lane (BVH8 entries are 2 words)
     uint32_t empty;        // no triangles
 };

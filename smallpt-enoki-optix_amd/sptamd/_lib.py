@@ -22,7 +22,7 @@ PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
 
 # Every function include/spt.h declares (the CPU test checks they are exported).
 EXPORTED = [
-    "spt_init", "spt_scene_create", "spt_scene_set_albedo", "spt_scene_get_stats",
+    "spt_init", "spt_scene_create", "spt_scene_set_albedo", "spt_scene_set_emission", "spt_scene_get_stats",
     "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
     "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write",
@@ -93,7 +93,8 @@ class Mesh(ctypes.Structure):
     _fields_ = [("pos_tri", POINTER(c_int32)), ("pos", POINTER(c_float)), ("nvert", c_uint64), ("ntri", c_uint64),
                 ("nrm_tri", POINTER(c_int32)), ("nrm", POINTER(c_float)), ("nnrm", c_uint64),
                 ("tc_tri", POINTER(c_int32)), ("tc", POINTER(c_float)), ("ntc", c_uint64),
-                ("mat_id", POINTER(c_int32)), ("kd", POINTER(c_float)), ("nmat", c_uint32)]
+                ("mat_id", POINTER(c_int32)), ("kd", POINTER(c_float)), ("nmat", c_uint32),
+                ("ke", POINTER(c_float))]
 
 
 def _load() -> ctypes.CDLL:
@@ -111,6 +112,7 @@ def _load() -> ctypes.CDLL:
         "spt_init": (i32, [i32]),
         "spt_scene_create": (i32, [vp, vp, u64, u64, vp, vp, u64, vp, vp, u64, vp, POINTER(vp)]),
         "spt_scene_set_albedo": (i32, [vp, vp, u32]),
+        "spt_scene_set_emission": (i32, [vp, vp, u32]),
         "spt_scene_get_stats": (i32, [vp, POINTER(SceneStats)]),
         "spt_scene_destroy": (i32, [vp]),
         "spt_intersect": (i32, [vp, POINTER(Rays), vp, u32, POINTER(Hits), u32, i32, vp]),

@@ -131,6 +131,10 @@ class HipBackend:
         a = np.ascontiguousarray(np.asarray(albedo_rgb, dtype=np.float32).reshape(-1, 3))
         check(lib.spt_scene_set_albedo(self._scene, a.ctypes.data, a.shape[0]), "spt_scene_set_albedo")
 
+    def set_emission(self, emission_rgb) -> None:
+        e = np.ascontiguousarray(np.asarray(emission_rgb, dtype=np.float32).reshape(-1, 3))
+        check(lib.spt_scene_set_emission(self._scene, e.ctypes.data, e.shape[0]), "spt_scene_set_emission")
+
     @property
     def handle(self):
         return self._scene
@@ -238,6 +242,8 @@ class Scene:
                                         m.get("tc"), m.get("mat_id"))
         if m.get("albedo") is not None:
             self.backend.set_albedo(m["albedo"])
+        if m.get("emission") is not None:
+            self.backend.set_emission(m["emission"])
 
     def intersect(self, ray: Ray3, active=None):           # main.cpp:320-340
         return self.backend.intersect(ray, active)

@@ -39,10 +39,12 @@ class _Builder:
         self.nn = 0
         self.mtl_names: List[str] = []
         self.kd: List[tuple] = []
+        self.ke: List[tuple] = []
 
-    def material(self, name: str, kd) -> int:
+    def material(self, name: str, kd, ke=(0.0, 0.0, 0.0)) -> int:
         self.mtl_names.append(name)
         self.kd.append(tuple(float(x) for x in kd))
+        self.ke.append(tuple(float(x) for x in ke))
         return len(self.mtl_names)  # obj index + 1
 
     def add(self, pos, nrm, pt, nt, mat: int):
@@ -60,8 +62,9 @@ class _Builder:
 
     def mesh(self) -> Dict[str, np.ndarray]:
         kd = np.array([(1.0, 1.0, 1.0)] + self.kd, np.float32)
+        ke = np.array([(0.0, 0.0, 0.0)] + self.ke, np.float32)
         return dict(pos=np.concatenate(self.pos), nrm=np.concatenate(self.nrm), pos_tri=np.concatenate(self.pt),
-                    nrm_tri=np.concatenate(self.nt), mat_id=np.concatenate(self.mat), kd=kd,
+                    nrm_tri=np.concatenate(self.nt), mat_id=np.concatenate(self.mat), kd=kd, ke=ke,
                     mtl_names=list(self.mtl_names))
 
 
@@ -97,6 +100,20 @@ def _sphere(center, r, nlon, nlat, keep=None, flip=False):
         n = -n
     # degenerate pole triangles are kept (zero area: the watertight test rejects them)
     return p, n, tris
+
+
+def _bottom_cap(center, r, theta_max, nseg, nring):
+    """Spherical cap around the -y pole of a sphere (polar angle <= theta_max),
+    outward normals."""
+    th = np.linspace(0.0, theta_max, nring + 1)[1:]
+    a = np.arange(nseg) * (2 * math.pi / nseg)
+    tt, aa = np.meshgrid(th, a, indexing="ij")
+    n = np.stack([np.sin(tt) * np.cos(aa), -np.cos(tt), np.sin(tt) * np.sin(aa)], -1).reshape(-1, 3)
+    n = np.concatenate([[[0.0, -1.0, 0.0]], n])
+    p = np.asarray(center, np.float64) + r * n
+    fan = np.stack([np.zeros(nseg, np.int64), 1 + np.arange(nseg), 1 + (np.arange(nseg) + 1) % nseg], -1)
+    rings, _ = _grid_tris(nseg, nring - 1, wrap_u=True)
+    return p, n, np.concatenate([fan, rings + 1])
 
 
 def _torus(center, R, r, nu, nv):
@@ -168,16 +185,21 @@ def mitsuba_synth(detail: float = 1.0) -> Dict[str, np.ndarray]:
 
 def cornell_spheres(detail: float = 1.0) -> Dict[str, np.ndarray]:
     """smallpt's Cornell box in smallpt units scaled by 1/100 (walls as quads,
-    the mirror/glass spheres made diffuse, ceiling light as a small disk).
+    the mirror/glass spheres made diffuse, ceiling light as a small cap with
+    Ke = 12 like smallpt's light sphere; the open front acts as smallpt's black
+    front wall when rendered with env = 0).  Render with smallpt_materials().
     Camera: cornell_camera()."""
     b = _Builder()
     m_left = b.material("left", (0.75, 0.25, 0.25))
     m_right = b.material("right", (0.25, 0.25, 0.75))
     m_white = b.material("white", (0.75, 0.75, 0.75))
     m_sph = b.material("sphere", (0.999, 0.999, 0.999))
-    m_light = b.material("light", (0.0, 0.0, 0.0))
+    m_light = b.material("light", (0.0, 0.0, 0.0), (12.0, 12.0, 12.0))
     s = lambda n: max(4, int(round(n * detail)))  # noqa: E731
-    x0, x1, y0, y1, z0, z1 = 0.01, 0.99, 0.0, 0.816, 0.0, 1.7
+    # smallpt's walls are planes (1e5 spheres) and its camera rays start 1.4
+    # units in (cam.o + d * 140): the side walls, floor and ceiling run out to
+    # z = 2.9 (just short of the camera) so every camera ray enters the box.
+    x0, x1, y0, y1, z0, z1 = 0.01, 0.99, 0.0, 0.816, 0.0, 2.9
     walls = [
         ((x0, y0, z0), (0, 0, z1 - z0), (0, y1 - y0, 0), (1, 0, 0), m_left),      # left
         ((x1, y0, z0), (0, y1 - y0, 0), (0, 0, z1 - z0), (-1, 0, 0), m_right),    # right
@@ -191,10 +213,18 @@ def cornell_spheres(detail: float = 1.0) -> Dict[str, np.ndarray]:
     for c in ((0.27, 0.165, 0.47), (0.73, 0.165, 0.78)):
         p, n, t = _sphere(c, 0.165, s(192), s(96))
         b.add(p, n, t, t, m_sph)
-    p, n, t = _sphere((0.5, 0.816 + 0.6 - 0.0027, 0.816), 0.6, s(128), s(64),
-                      keep=lambda lon, lat: lat < math.radians(-80))
+    # smallpt: Sphere(600, Vec(50, 681.6 - .27, 81.6), Vec(12, 12, 12)) — only
+    # the part below the ceiling (a disk of radius ~0.18) is visible.
+    p, n, t = _bottom_cap((0.5, 6.816 - 0.0027, 0.816), 6.0, math.radians(2.5), s(64), s(8))
     b.add(p, n, t, t, m_light)
     return b.mesh()
+
+
+def smallpt_materials(mesh: Dict[str, np.ndarray]):
+    """(albedo, emission) tables for smallpt-style shading: Kd as albedo and Ke
+    as emission (the reference itself renders albedo 1, no emitters)."""
+    ke = mesh.get("ke")
+    return mesh["kd"], (ke if ke is not None else np.zeros_like(mesh["kd"]))
 
 
 def cornell_camera() -> dict:
@@ -248,7 +278,11 @@ def write_obj(path: str, mesh: Dict[str, np.ndarray], mtl: str = None) -> None:
     with open(mtl, "w") as f:
         for i, nm in enumerate(names):
             kd = mesh["kd"][i + 1]
-            f.write(f"newmtl {nm}\nKd {kd[0]:.6g} {kd[1]:.6g} {kd[2]:.6g}\n\n")
+            f.write(f"newmtl {nm}\nKd {kd[0]:.6g} {kd[1]:.6g} {kd[2]:.6g}\n")
+            ke = mesh["ke"][i + 1] if mesh.get("ke") is not None else (0.0, 0.0, 0.0)
+            if any(float(x) != 0.0 for x in ke):
+                f.write(f"Ke {ke[0]:.6g} {ke[1]:.6g} {ke[2]:.6g}\n")
+            f.write("\n")
     pos, nrm = mesh["pos"], mesh["nrm"]
     pt, nt, mat = mesh["pos_tri"], mesh["nrm_tri"], mesh["mat_id"]
     with open(path, "w") as f:
@@ -288,6 +322,7 @@ def load_obj(path: str) -> Dict[str, np.ndarray]:
             tc=_np_copy(m.tc, 2 * m.ntc, np.float32).reshape(-1, 2),
             mat_id=_np_copy(m.mat_id, m.ntri, np.int32),
             kd=_np_copy(m.kd, 3 * m.nmat, np.float32).reshape(-1, 3),
+            ke=_np_copy(m.ke, 3 * m.nmat, np.float32).reshape(-1, 3),
         )
     finally:
         _lib.lib.spt_mesh_free(ctypes.byref(m))

@@ -152,3 +152,54 @@ def test_gpu_matches_committed_golden():
     np.testing.assert_array_equal(t.cpu().numpy()[h], g["isect_t"][h])
     s.backend.set_albedo(g["albedo"])
     np.testing.assert_array_equal(gpu_render(s, 20, 16, 6, 6, rr_start_depth=2)[0], g["film_albedo_rr2"])
+
+
+@pytest.fixture(scope="module")
+def cornell():
+    """smallpt's Cornell box (BASELINE config 3): Kd albedo, Ke = 12 light, black sky."""
+    m = scenes.cornell_spheres(detail=0.25)
+    alb, emi = scenes.smallpt_materials(m)
+    s = sptamd.Scene()
+    s.add_arrays(m)
+    s.commit(0)
+    s.backend.set_albedo(alb)
+    s.backend.set_emission(emi)
+    return s, O.OracleScene(m, albedo=alb, emission=emi)
+
+
+@pytest.mark.parametrize("wavefront", [0, 777])
+def test_cornell_emission_bitexact(cornell, wavefront):
+    """Emitters: each path carries its gathered radiance and writes it once per
+    (sample, pixel); the last cast is a closest hit (it must see the light)."""
+    s, osc = cornell
+    kw = dict(camera=scenes.cornell_camera(), rr_start_depth=5, env=(0.0, 0.0, 0.0))
+    got, st = gpu_render(s, 48, 40, 8, 10, wavefront_paths=wavefront, **kw)
+    ref, casts = oracle_render(osc, 48, 40, 8, 10, **kw)
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+    assert got.max() >= 12.0 / 8  # the light is in view
+
+
+def test_emission_with_sky_and_albedo(mesh):
+    """Emitters, non-unit albedo, roulette and a coloured sky together."""
+    s = sptamd.Scene()
+    s.add_arrays(mesh)
+    s.commit(0)
+    nm = len(mesh["kd"])
+    albedo = np.full((nm, 3), 0.7, np.float32)
+    emi = np.zeros((nm, 3), np.float32)
+    emi[1] = (2.0, 1.0, 0.5)
+    emi[nm - 1] = (0.0, 0.3, 3.0)
+    s.backend.set_albedo(albedo)
+    s.backend.set_emission(emi)
+    osc = O.OracleScene(mesh, albedo=albedo, emission=emi)
+    kw = dict(rr_start_depth=3, env=(0.5, 0.75, 1.0))
+    got, st = gpu_render(s, 40, 30, 6, 7, **kw)
+    ref, casts = oracle_render(osc, 40, 30, 6, 7, **kw)
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+    # clearing the emission table restores the any-hit last cast and the plain image
+    s.backend.set_emission(np.zeros((nm, 3), np.float32))
+    got0, _ = gpu_render(s, 40, 30, 6, 7, **kw)
+    ref0, _ = oracle_render(O.OracleScene(mesh, albedo=albedo), 40, 30, 6, 7, **kw)
+    np.testing.assert_array_equal(got0, ref0)

@@ -59,7 +59,7 @@ def _write(path, text):
 
 
 def test_obj_loader_semantics(tmp_path):
-    _write(tmp_path / "m.mtl", "newmtl red\nKd 0.9 0.1 0.1\n\nnewmtl blue\nKd 0.1 0.1 0.9\n")
+    _write(tmp_path / "m.mtl", "newmtl red\nKd 0.9 0.1 0.1\n\nnewmtl blue\nKd 0.1 0.1 0.9\nKe 4 5 6\n")
     _write(tmp_path / "a.obj", """# test
 mtllib m.mtl
 v 0 0 0
@@ -87,6 +87,7 @@ f -1 -2 -3
     # obj material id + 1 (main.cpp:185): none -> 0, blue (index 1) -> 2, red (0) -> 1, unknown -> 0
     np.testing.assert_array_equal(m["mat_id"], [0, 2, 1, 1, 0])
     np.testing.assert_allclose(m["kd"], [[1, 1, 1], [0.9, 0.1, 0.1], [0.1, 0.1, 0.9]])
+    np.testing.assert_allclose(m["ke"], [[0, 0, 0], [0, 0, 0], [4, 5, 6]])  # Ke: emission table
     assert m["pos"].shape == (5, 3) and m["nrm"].shape == (2, 3) and m["tc"].shape == (3, 2)
 
 
@@ -106,6 +107,12 @@ def test_generated_scene_roundtrip(tmp_path):
         np.testing.assert_array_equal(l[k], m[k])
     for k in ("pos", "nrm", "kd"):
         np.testing.assert_array_equal(l[k], m[k].astype(np.float32))
+    c = scenes.cornell_spheres(detail=0.25)
+    scenes.write_obj(path, c)
+    l = scenes.load_obj(path)
+    np.testing.assert_array_equal(l["mat_id"], c["mat_id"])
+    np.testing.assert_array_equal(l["ke"], c["ke"])
+    assert l["ke"].max() == 12.0
 
 
 def test_pfm_writer(tmp_path):

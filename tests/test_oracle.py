@@ -226,6 +226,36 @@ def test_analytic_closed_box():
     assert np.all(f == 0.0) and casts == 16 * 16 * 2 * 5
 
 
+def test_emissive_closed_box_geometric_series():
+    """Every wall emits Le = 1 with albedo 1/2 and nothing escapes: with D casts
+    and no roulette each sample gathers 1 + 1/2 + ... + 2^(1-D), exact in fp32."""
+    c = np.array([[x, y, z] for x in (-20, 20) for y in (-20, 20) for z in (-20, 20)], np.float32)
+    quads = [(0, 1, 3, 2), (4, 6, 7, 5), (0, 4, 5, 1), (2, 3, 7, 6), (0, 2, 6, 4), (1, 5, 7, 3)]
+    tris = np.array([t for a, b, cc, d in quads for t in ((a, b, cc), (a, cc, d))], np.int32)
+    nrm = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float32)
+    nt = np.repeat(np.arange(6, dtype=np.int32), 2)[:, None].repeat(3, 1)
+    mesh = {"pos": c, "pos_tri": tris, "nrm": nrm, "nrm_tri": nt, "mat_id": np.ones(12, np.int32)}
+    sc = O.OracleScene(mesh, albedo=[[1, 1, 1], [0.5, 0.5, 0.5]], emission=[[0, 0, 0], [1, 1, 1]])
+    for depth in (1, 4, 7):
+        f, casts = sc.render(O.reference_params(12, 10, 3, depth, rr_start_depth=depth))
+        assert casts == 12 * 10 * 3 * depth
+        assert np.all(f == np.float32(2.0 - 2.0 ** (1 - depth))), depth
+
+
+def test_emission_off_material_and_sky_sum():
+    """Emitters on one material, sky on: each sample is its emitted hits plus
+    the sky term; with emission all zero the image equals the reference's."""
+    m = scenes.mitsuba_synth(detail=0.1)
+    p = O.reference_params(24, 20, 4, 4)
+    base, _ = O.OracleScene(m).render(p)
+    zero, _ = O.OracleScene(m, emission=np.zeros((len(m["kd"]), 3), np.float32)).render(p)
+    np.testing.assert_array_equal(base, zero)
+    emi = np.zeros((len(m["kd"]), 3), np.float32)
+    emi[1] = (0.5, 0.25, 0.0)
+    lit, _ = O.OracleScene(m, emission=emi).render(p)
+    assert np.all(lit >= base) and np.any(lit[0] > base[0]) and np.all(lit[2] == base[2])
+
+
 def test_film_is_escape_fraction():
     """Albedo 1, sky 1: every pixel is an exact count / spp, R=G=B."""
     sc = O.OracleScene(scenes.mitsuba_synth(detail=0.1))

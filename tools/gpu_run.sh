@@ -29,6 +29,8 @@ for s in "$@"; do
     tests2) run tests2 900 env SPT_BVH=2 python -m pytest tests -m gpu -q -x ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench2|bench3|bench4) run $s 600 python bench.py --config ${s#bench} --steps 2 --warmup 1 ;;
+    bench2q|bench3q|bench4q) c=${s#bench}; run $s 600 python bench.py --config ${c%q} --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchwf) for wf in ${WFS:-1048576 4194304 8388608}; do run benchwf$wf 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --wavefront $wf; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
