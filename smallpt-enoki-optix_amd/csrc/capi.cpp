@@ -63,17 +63,25 @@ double now_ms() {
 constexpr size_t kPathBytes = 8 + 6 * 4 + 4 + 4 + 3 * 4 + 3 * 4;
 constexpr size_t kHitBytes = 16;
 
-PathQueue carve_queue(char* base, size_t cap) {
+// Planes are `stride` elements apart (stride = cap + pad, see queue_stride).
+PathQueue carve_queue(char* base, size_t stride) {
     PathQueue q;
     q.rng = (uint64_t*)base;
-    float* f = (float*)(base + 8 * cap);
-    q.ox = f; q.oy = f + cap; q.oz = f + 2 * cap;
-    q.dx = f + 3 * cap; q.dy = f + 4 * cap; q.dz = f + 5 * cap;
-    q.pix = (uint32_t*)(f + 6 * cap);
-    q.meta = q.pix + cap;
-    q.tr = (float*)(q.meta + cap); q.tg = q.tr + cap; q.tb = q.tg + cap;
-    q.lr = q.tb + cap; q.lg = q.lr + cap; q.lb = q.lg + cap;
+    float* f = (float*)(base + 8 * stride);
+    q.ox = f; q.oy = f + stride; q.oz = f + 2 * stride;
+    q.dx = f + 3 * stride; q.dy = f + 4 * stride; q.dz = f + 5 * stride;
+    q.pix = (uint32_t*)(f + 6 * stride);
+    q.meta = q.pix + stride;
+    q.tr = (float*)(q.meta + stride); q.tg = q.tr + stride; q.tb = q.tg + stride;
+    q.lr = q.tb + stride; q.lg = q.lr + stride; q.lb = q.lg + stride;
     return q;
+}
+
+// Plane stride: cap plus a pad so the SoA planes (and the two queues) do not
+// sit a power of two apart.
+size_t queue_stride(size_t cap) {
+    static const uint32_t pad = env_u32("SPT_PLANE_PAD", 0, 0, 1u << 20);
+    return cap + pad;
 }
 
 // Device counters of one sub-wavefront (zeroed per chunk; see spt_render).
@@ -213,8 +221,8 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, size_t film_flo
         if (cap > b.cap) {
             hfree(b.qa); hfree(b.qb); hfree(b.hits);
             b.cap = 0;
-            HIP_TRY(hipMalloc((void**)&b.qa, kPathBytes * cap));
-            HIP_TRY(hipMalloc((void**)&b.qb, kPathBytes * cap));
+            HIP_TRY(hipMalloc((void**)&b.qa, kPathBytes * queue_stride(cap)));
+            HIP_TRY(hipMalloc((void**)&b.qb, kPathBytes * queue_stride(cap)));
             HIP_TRY(hipMalloc((void**)&b.hits, kHitBytes * cap));
             b.cap = cap;
         }
@@ -598,8 +606,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     PathQueue q[kMaxStreams][2];
     for (int k = 0; k < K; k++) {
         Sub& b = ws.sub[k];
-        q[k][0] = carve_queue(b.qa, b.cap);
-        q[k][1] = carve_queue(b.qb, b.cap);
+        q[k][0] = carve_queue(b.qa, queue_stride(b.cap));
+        q[k][1] = carve_queue(b.qb, queue_stride(b.cap));
         IsectQueueArgs& I = ia[k];
         I.sc = sc->dev();
         I.hits = (float4*)b.hits;
@@ -627,6 +635,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
         R.initstate = p.rng_initstate;
+        R.carry_l = sc->emission != nullptr;
         R.isect_next = &b.cnt->isect_next;
     }
 

@@ -377,14 +377,16 @@ __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32
 
 __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix,
                                            uint32_t meta, uint64_t rng, float tr, float tg, float tb, float lr,
-                                           float lg, float lb) {
+                                           float lg, float lb, bool with_l) {
     q.ox[j] = o.x; q.oy[j] = o.y; q.oz[j] = o.z;
     q.dx[j] = d.x; q.dy[j] = d.y; q.dz[j] = d.z;
     q.pix[j] = pix;
     q.meta[j] = meta;
     q.rng[j] = rng;
     q.tr[j] = tr; q.tg[j] = tg; q.tb[j] = tb;
-    q.lr[j] = lr; q.lg[j] = lg; q.lb[j] = lb;
+    if (with_l) {  // gathered radiance planes: only scenes with emitters use them
+        q.lr[j] = lr; q.lg[j] = lg; q.lb[j] = lb;
+    }
 }
 
 // Refill: start work items [cursor, cursor + total) in queue slots
@@ -418,7 +420,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     V3 o, d;
     camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
     store_path(a.q, surv + i, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f,
-               0.0f);  // main.cpp:391
+               0.0f, a.carry_l);  // main.cpp:391
 }
 
 // ----------------------------------------------------------------- shade
@@ -426,6 +428,8 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 // writes its one contribution (throughput x sky radiance on escape, else 0)
 // to sfilm[sample][c][pixel]; survivors are compacted into the out queue with
 // a wave ballot + mbcnt rank and one atomicAdd per block.
+// kEmit: the scene has emitters (gathered radiance carried in the queue).
+template <bool kEmit>
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
@@ -449,14 +453,14 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         const float4 hit = a.hits[i];
         const int32_t slot = (int32_t)f2u(hit.x);
         tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
-        lr = a.in.lr[i]; lg = a.in.lg[i]; lb = a.in.lb[i];
+        if (kEmit) { lr = a.in.lr[i]; lg = a.in.lg[i]; lb = a.in.lb[i]; }
         bool term = true;
         if (slot < 0) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
             lr = lr + tr * a.env_r;
             lg = lg + tg * a.env_g;
             lb = lb + tb * a.env_b;
-        } else if (a.sc.emission) {
+        } else if (kEmit) {
             // emitted radiance at the hit (smallpt obj.e; not in the reference)
             uint32_t mat = f2u(a.sc.snrm[(size_t)slot * 3].w);
             if (mat < a.sc.nemit) {
@@ -545,7 +549,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
     }
     __syncthreads();
-    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb, lr, lg, lb);
+    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb, lr, lg, lb, kEmit);
 }
 
 // Per-pixel sum of the per-sample contributions in sample order
@@ -661,7 +665,10 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
 
 hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
-    hipLaunchKernelGGL(shade_kernel, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
+    if (a.sc.emission)
+        hipLaunchKernelGGL(shade_kernel<true>, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(shade_kernel<false>, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
     return hipGetLastError();
 }
 

@@ -96,6 +96,7 @@ struct RefillArgs {
     uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     uint64_t initstate;
+    bool carry_l;               // write the gathered-radiance planes (emitters present)
 };
 
 struct HitInfoArgs {
