@@ -11,7 +11,8 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_uint8, c_uin
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "build", "libspt.so")
+# SPT_LIB: a variant build of the same library (A/B experiments, tools/ab.sh)
+LIB_PATH = os.environ.get("SPT_LIB") or os.path.join(PKG_ROOT, "build", "libspt.so")
 
 SPT_OK = 0
 SPT_RNG_Y_FIRST = 0
