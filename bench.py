@@ -72,9 +72,8 @@ def workload(args, scenes):
     cast 5, smallpt's camera; otherwise the reference's semantics (albedo 1,
     sky 1, main.cpp:383 camera)."""
     if args.scene == "city_synth":  # 10M triangles: arrays, not a 600 MB OBJ
-        src = scenes.city_synth(10_000_000)
-    else:
-        src = scenes.scene_obj(args.scene)
+        return scenes.city_synth(10_000_000), dict(camera=scenes.city_camera()), None, None
+    src = scenes.scene_obj(args.scene)
     if not args.smallpt:
         return src, {}, None, None
     kw = dict(camera=scenes.cornell_camera(), rr_start_depth=5, env=(0.0, 0.0, 0.0))

@@ -271,6 +271,12 @@ def city_synth(target_tris: int = 10_000_000, seed: int = 7) -> Dict[str, np.nda
     return b.mesh()
 
 
+def city_camera() -> dict:
+    """A courtyard view for city_synth (San Miguel comes with its own pbrt camera)."""
+    return dict(look_from=(-6.0, 2.5, 8.0), look_at=(2.0, 0.5, -4.0), up=(0.0, 1.0, 0.0), lens_radius=0.0,
+                focal_dist=1.0, fov_y=0.9, film_size_y=0.035)
+
+
 def write_obj(path: str, mesh: Dict[str, np.ndarray], mtl: str = None) -> None:
     """Write mesh as OBJ (+ .mtl) using v / vn / f v//vn and usemtl groups."""
     mtl = mtl or os.path.splitext(path)[0] + ".mtl"

@@ -203,3 +203,19 @@ def test_emission_with_sky_and_albedo(mesh):
     got0, _ = gpu_render(s, 40, 30, 6, 7, **kw)
     ref0, _ = oracle_render(O.OracleScene(mesh, albedo=albedo), 40, 30, 6, 7, **kw)
     np.testing.assert_array_equal(got0, ref0)
+
+
+def test_city_scene_bitexact():
+    """The config-5 generator (10M-triangle courtyard) at 300k triangles: a
+    deeper, wider BVH8 than mitsuba_synth, same bits as the oracle."""
+    m = scenes.city_synth(300_000)
+    s = sptamd.Scene()
+    s.add_arrays(m)
+    s.commit(0)
+    osc = O.OracleScene(m)
+    cam = scenes.city_camera()
+    got, st = gpu_render(s, 64, 36, 4, 8, camera=cam)
+    ref, casts = oracle_render(osc, 64, 36, 4, 8, camera=cam)
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+    assert 0.0 < got.mean() < 1.0
