@@ -425,10 +425,13 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 
 // ----------------------------------------------------------------- shade
 // main.cpp:404-425 for one cast of every queued path.  A path that ends
-// writes its one contribution (throughput x sky radiance on escape, else 0)
-// to sfilm[sample][c][pixel]; survivors are compacted into the out queue with
-// a wave ballot + mbcnt rank and one atomicAdd per block.
-// kEmit: the scene has emitters (gathered radiance carried in the queue).
+// writes its gathered radiance (throughput x sky radiance on escape, plus
+// emitted radiance with emitters) to sfilm[sample][c][pixel]; survivors are
+// compacted into the out queue with a wave ballot + mbcnt rank and one
+// atomicAdd per block.  Phase 1 decides which paths survive (miss, last cast,
+// albedo, roulette) from the hit and the material word alone, so the block's
+// queue atomic is issued before phase 2 (new ray: RNG draw, interpolated
+// normal, Frame3, cosine sample) and its latency hides behind that work.
 template <bool kEmit>
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
@@ -438,19 +441,20 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     const uint32_t i = blockIdx.x * kShadeBlock + tid;
     const uint32_t n = *a.count_in;
     if (tid < 2) s_stats[tid] = 0;
-    __syncthreads();
 
+    // ---- phase 1: survive or terminate (the bounce inputs load alongside)
     bool emit = false;
-    V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
-    uint32_t pix = 0, nmeta = 0;
-    uint64_t nrng = 0;
+    uint32_t pix = 0, meta = 0, gpix = 0;
+    float4 hit = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m0 = hit, m1 = hit, m2 = hit;
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
+    uint64_t rs = 0;
     if (i < n) {
         pix = a.in.pix[i];
-        const uint32_t meta = a.in.meta[i];
+        meta = a.in.meta[i];
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
-        const float4 hit = a.hits[i];
+        hit = a.hits[i];
         const int32_t slot = (int32_t)f2u(hit.x);
         tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
         if (kEmit) { lr = a.in.lr[i]; lg = a.in.lg[i]; lb = a.in.lb[i]; }
@@ -460,62 +464,45 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             lr = lr + tr * a.env_r;
             lg = lg + tg * a.env_g;
             lb = lb + tb * a.env_b;
-        } else if (kEmit) {
-            // emitted radiance at the hit (smallpt obj.e; not in the reference)
-            uint32_t mat = f2u(a.sc.snrm[(size_t)slot * 3].w);
-            if (mat < a.sc.nemit) {
+        } else {
+            const bool bounce = depth + 1 < a.max_depth;
+            m0 = a.sc.snrm[(size_t)slot * 3];  // n0 + material id
+            if (bounce) {
+                m1 = a.sc.snrm[(size_t)slot * 3 + 1];
+                m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+                rs = a.in.rng[i];
+                o = v3(a.in.ox[i], a.in.oy[i], a.in.oz[i]);
+                d = v3(a.in.dx[i], a.in.dy[i], a.in.dz[i]);
+            }
+            uint32_t mat = f2u(m0.w);
+            if (kEmit && mat < a.sc.nemit) {
+                // emitted radiance at the hit (smallpt obj.e; not in the reference)
                 lr = lr + tr * a.sc.emission[mat * 3];
                 lg = lg + tg * a.sc.emission[mat * 3 + 1];
                 lb = lb + tb * a.sc.emission[mat * 3 + 2];
             }
-        }
-        if (slot >= 0 && depth + 1 < a.max_depth) {
-            const uint32_t lx = pix % a.W, ly = pix / a.W;
-            const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
-            const uint32_t gpix = gy * a.W + lx;
-            Pcg32 rng;
-            rng.state = a.in.rng[i];
-            rng.inc = ((uint64_t)gpix << 1u) | 1u;
-            const V3 o = v3(a.in.ox[i], a.in.oy[i], a.in.oz[i]);
-            const V3 d = v3(a.in.dx[i], a.in.dy[i], a.in.dz[i]);
-            const float t = hit.y, u = hit.z, v = hit.w;
-            float xi_x, xi_y;
-            draw2(rng, a.rng_order, xi_x, xi_y);               // main.cpp:413
-            const float4 m0 = a.sc.snrm[(size_t)slot * 3];
-            const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
-            const float4 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
-            const float w = (1.0f - u) - v;                      // add_math.h:6
-            const V3 sn = v3((w * m0.x + u * m1.x) + v * m2.x,  // optix_backend.h:483-484
-                             (w * m0.y + u * m1.y) + v * m2.y,
-                             (w * m0.z + u * m1.z) + v * m2.z);
-            const V3 hp = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);  // optix_backend.h:469
-            const Frame fr = frame_from_normal(sn);              // main.cpp:414
-            const V3 out = to_world(fr, cosine_hemisphere(xi_x, xi_y));  // main.cpp:418-419
-            uint32_t mat = f2u(m0.w);
-            if (mat >= a.sc.nmat) mat = 0;
-            tr = tr * a.sc.albedo[mat * 3];                      // main.cpp:422
-            tg = tg * a.sc.albedo[mat * 3 + 1];
-            tb = tb * a.sc.albedo[mat * 3 + 2];
-            term = false;
-            if (depth + 1 >= a.rr_start) {
-                const float q = fmaxf(tr, fmaxf(tg, tb));
-                if (q < 1.0f) {
-                    if (rr_uniform(gpix, sample, depth) >= q) {
-                        term = true;
-                    } else {
-                        tr = tr / q; tg = tg / q; tb = tb / q;
+            if (bounce) {
+                const uint32_t lx = pix % a.W, ly = pix / a.W;
+                gpix = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group) * a.W + lx;
+                if (mat >= a.sc.nmat) mat = 0;
+                tr = tr * a.sc.albedo[mat * 3];                  // main.cpp:422
+                tg = tg * a.sc.albedo[mat * 3 + 1];
+                tb = tb * a.sc.albedo[mat * 3 + 2];
+                term = false;
+                if (depth + 1 >= a.rr_start) {
+                    const float q = fmaxf(tr, fmaxf(tg, tb));
+                    if (q < 1.0f) {
+                        if (rr_uniform(gpix, sample, depth) >= q) {
+                            term = true;
+                        } else {
+                            tr = tr / q; tg = tg / q; tb = tb / q;
+                        }
                     }
                 }
             }
-            if (!term) {
-                emit = true;
-                no = hp;                                          // main.cpp:423
-                nd = out;                                         // main.cpp:424
-                nmeta = meta + 1u;
-                nrng = rng.state;
-            }
+            // else: hit on the last cast — the path ends (no sky contribution).
         }
-        // else: hit on the last cast — the path ends without contribution.
+        emit = !term;
         if (term) {
             float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
             f[0] = lr;
@@ -524,32 +511,56 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
     }
 
-    // Compaction: wave ballot + mbcnt rank, one atomicAdd per block.
+    // ---- compaction: wave ballot + mbcnt rank, one queue atomic per block
     const uint64_t ball = __ballot(emit);
     const uint32_t rank =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
     const uint64_t bi = __ballot(i < n);
+    __syncthreads();  // s_stats initialised
     if (lane == 0) {
         s_wave_cnt[wave] = (uint32_t)__popcll(ball);
         atomicAdd(&s_stats[0], (uint32_t)__popcll(bi));
         atomicAdd(&s_stats[1], (uint32_t)__popcll(ball));
     }
     __syncthreads();
+    uint32_t base = 0, total = 0;
     if (tid == 0) {
-        uint32_t total = 0;
-        for (uint32_t w = 0; w < kShadeBlock / 64; w++) {
-            s_wave_off[w] = total;
-            total += s_wave_cnt[w];
-        }
-        const uint32_t base = total ? atomicAdd(a.count_out, total) : 0u;
-        for (uint32_t w = 0; w < kShadeBlock / 64; w++) s_wave_off[w] += base;
+        for (uint32_t w = 0; w < kShadeBlock / 64; w++) total += s_wave_cnt[w];
+        if (total) base = atomicAdd(a.count_out, total);  // returns during phase 2
         if (s_stats[0]) {
             atomicAdd(&a.stats[0], (unsigned long long)s_stats[0]);
             if (s_stats[1]) atomicAdd(&a.stats[1], (unsigned long long)s_stats[1]);
         }
     }
+
+    // ---- phase 2: the bounce ray of every survivor
+    V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
+    uint64_t nrng = 0;
+    if (emit) {
+        Pcg32 rng;
+        rng.state = rs;
+        rng.inc = ((uint64_t)gpix << 1u) | 1u;
+        const float t = hit.y, u = hit.z, v = hit.w;
+        float xi_x, xi_y;
+        draw2(rng, a.rng_order, xi_x, xi_y);                   // main.cpp:413
+        const float w = (1.0f - u) - v;                          // add_math.h:6
+        const V3 sn = v3((w * m0.x + u * m1.x) + v * m2.x,      // optix_backend.h:483-484
+                         (w * m0.y + u * m1.y) + v * m2.y,
+                         (w * m0.z + u * m1.z) + v * m2.z);
+        no = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);   // optix_backend.h:469, main.cpp:423
+        const Frame fr = frame_from_normal(sn);                  // main.cpp:414
+        nd = to_world(fr, cosine_hemisphere(xi_x, xi_y));        // main.cpp:418-419, 424
+        nrng = rng.state;
+    }
+    if (tid == 0) {
+        uint32_t off = base;
+        for (uint32_t w = 0; w < kShadeBlock / 64; w++) {
+            s_wave_off[w] = off;
+            off += s_wave_cnt[w];
+        }
+    }
     __syncthreads();
-    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, nmeta, nrng, tr, tg, tb, lr, lg, lb, kEmit);
+    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, nrng, tr, tg, tb, lr, lg, lb, kEmit);
 }
 
 // Per-pixel sum of the per-sample contributions in sample order

@@ -11,7 +11,10 @@ namespace spt {
 constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kNode8Quads = 8;         // BVH8 node stride in 16-B units (80 B used, padded to one 128-B line)
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
-constexpr uint32_t kShadeBlock = 1024;      // shade: 16 waves, one queue atomic per block
+#ifndef SPT_SHADE_BLOCK
+#define SPT_SHADE_BLOCK 512
+#endif
+constexpr uint32_t kShadeBlock = SPT_SHADE_BLOCK;  // shade: 8 waves, one queue atomic per block (A/B: 256 / 512 / 1024)
 constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
 constexpr uint32_t kIsectChunk = 128;       // dynamic-share queue indices a wave takes per atomic
 constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
