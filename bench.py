@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--scene", default="")
     ap.add_argument("--rows-per-group", type=int, default=8)
     ap.add_argument("--wavefront", type=int, default=0, help="paths in flight per launch (0 = auto)")
+    ap.add_argument("--pipeline", choices=["wavefront", "fused"], default="wavefront",
+                    help="isect/shade/refill kernels over path queues (north-star design) or one fused "
+                         "persistent trace+shade kernel")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,7 +158,7 @@ def main():
     W, H = args.width, args.height
     R = args.rows_per_group
     params = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
-                                wavefront_paths=args.wavefront, timing=True, **kw)
+                                wavefront_paths=args.wavefront, timing=True, pipeline=args.pipeline, **kw)
     dev = torch.device("cuda", local)
     tg = TileGather(H, W, rank, world, R, dev)
     film = tg.tile_view()
@@ -220,7 +223,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
-            "config": {"workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
+            "config": {"pipeline": args.pipeline,
+                       "workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
@@ -228,7 +232,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "isect_queue_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "kernel": "isect_queue_kernel" if args.pipeline == "wavefront" else "render_fused_kernel", "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
                          "grays_per_s": round(agg["ray_casts"] / (agg["isect_ms"] * 1e-3) / 1e9, 4)
                          if agg["isect_ms"] else None},

@@ -76,7 +76,9 @@ enum {
 
 enum {
     SPT_FLAG_TIMING = 1u,          /* record HIP events around every isect/shade launch */
-    SPT_FLAG_TRAVERSAL_STATS = 2u  /* count node visits / triangle tests (slower variant) */
+    SPT_FLAG_TRAVERSAL_STATS = 2u, /* count node visits / triangle tests (slower variant; wavefront) */
+    SPT_FLAG_FUSED = 4u,           /* one persistent trace+shade kernel per sample chunk */
+    SPT_FLAG_WAVEFRONT = 8u        /* isect / shade / refill kernels over path queues */
 };
 
 /* The render loop of main.cpp:354-429 plus the tile/wavefront knobs. */

@@ -542,6 +542,14 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     }
     if (!film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
 
+    // Pipeline: the wavefront (isect / shade / refill over path queues, the
+    // north-star design) or the fused persistent kernel.  Traversal counters
+    // exist in the wavefront isect kernel only.
+    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
+    bool fused = env_u32("SPT_FUSED", 0, 0, 1) != 0;
+    if (p.flags & SPT_FLAG_FUSED) fused = true;
+    if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
+
     // Wavefront capacity.  Each isect launch ends in a tail where its last rays
     // finish while most lanes idle; 8M paths in flight (~1 GB of queues)
     // amortise it (measured: 1M 913, 2M 1191, 8M 1792 Mpaths/s on MI355X).
@@ -551,7 +559,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
                                        (unsigned long long)C);
     // The wavefront is split into K sub-wavefronts on their own streams, so one
     // sub-wavefront's launch tail overlaps the others' work.
-    int K = (int)env_u32("SPT_STREAMS", 2, 1, kMaxStreams);
+    int K = fused ? 1 : (int)env_u32("SPT_STREAMS", 2, 1, kMaxStreams);
+    if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
     // Per-sample contribution film [chunk][3][P], at most ~4 GiB per chunk.
@@ -562,7 +571,6 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     if (st) return st;
     Workspace& ws = sc->ws;
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
-    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
 
     // PCG32 jump to each sample's first draw: s * (4 + 2D) (main.cpp:395,396,413).
     const uint64_t per_sample = 4ull + 2ull * p.max_depth;
@@ -640,7 +648,42 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     }
 
     uint64_t iters = 0;
-    for (uint32_t s0 = 0; s0 < p.spp; s0 += chunk) {
+    if (fused) {
+        FusedArgs F;
+        F.sc = sc->dev();
+        F.cam = cam;
+        F.sample_jump = ws.jumps;
+        F.sfilm = sfilm;
+        F.stats = ws.stats->stats;
+        F.next = &ws.sub[0].cnt->isect_next;
+        F.initstate = p.rng_initstate;
+        F.P = (uint32_t)P; F.W = p.width; F.max_depth = p.max_depth;
+        F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
+        F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
+        F.refill_idle = env_u32("SPT_FUSED_IDLE", 32, 1, 64);
+        F.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 160, 0, 255);
+        F.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
+        F.grid_q8 = env_u32("SPT_FUSED_GRID_Q8", 256, 0, 4096);
+        F.env_r = p.env[0]; F.env_g = p.env[1]; F.env_b = p.env[2];
+        uint32_t lanes = 0;
+        for (uint32_t s0 = 0; s0 < p.spp; s0 += chunk) {
+            const uint32_t ns = std::min(chunk, p.spp - s0);
+            F.work0 = (uint64_t)s0 * P;
+            F.count = (uint32_t)((uint64_t)ns * P);  // <= 4 GiB / 12 B per chunk
+            F.sample0 = s0;
+            HIP_TRY(hipMemsetAsync(F.next, 0, sizeof(uint32_t), stream));
+            if ((st = mark(1, stream, [&] { return launch_fused(F, stream, &lanes); }))) return st;
+            if ((st = mark(3, stream, [&] {
+                     return launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
+                                           stream);
+                 })))
+                return st;
+            iters++;
+        }
+        C = lanes;
+        rs.paths_in_flight = lanes;
+    }
+    for (uint32_t s0 = 0; s0 < p.spp && !fused; s0 += chunk) {
         const uint32_t ns = std::min(chunk, p.spp - s0);
         const uint64_t w0 = (uint64_t)s0 * P, L = (uint64_t)ns * P;
         // fork: the sub-wavefront streams start after everything queued so far

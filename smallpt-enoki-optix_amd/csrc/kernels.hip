@@ -563,6 +563,169 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, nrng, tr, tg, tb, lr, lg, lb, kEmit);
 }
 
+// ------------------------------------------------------------ fused render
+// The whole of main.cpp:385-426 in one persistent launch per sample chunk:
+// each lane owns one path from its camera ray to termination.  Lanes whose
+// ray has finished wait (as "pending") until at least refill_idle lanes of
+// the wave are not tracing; then the wave shades all pending lanes at once
+// (same arithmetic as shade_kernel) and starts new paths (same as
+// refill_kernel) in the lanes that became free.  Path state never leaves the
+// registers, so there are no queues, compaction or per-bounce launches.  The
+// per-(sample, pixel) film writes are the same, so the image is bit-identical.
+#ifndef SPT_FUSED_WAVES
+#define SPT_FUSED_WAVES 6
+#endif
+template <typename Tr, bool kEmit>
+__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
+void render_fused_kernel(FusedArgs a) {
+    extern __shared__ uint32_t lds_stack[];
+    uint32_t* stk = lds_stack + threadIdx.x;
+    const uint32_t n = a.count;
+    NoStats st;
+    Tr tr;
+    V3 dir = v3(0, 0, 0);
+    uint64_t rs = 0;
+    uint32_t pix = 0, gpix = 0, sample = 0, depth = 0;
+    float thr = 1.0f, thg = 1.0f, thb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
+    bool busy = false, pending = false;
+    uint32_t casts = 0, conts = 0, starts = 0;
+    // wave-uniform work pool: static share, then dynamic chunks
+    const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
+    const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
+    const uint32_t dyn_base = share * nwaves;
+    uint32_t pool = wave_id * share, pool_end = pool + share;
+    bool drained = false;
+    while (true) {
+        if ((uint32_t)__popcll(__ballot(!busy)) >= a.refill_idle) {
+            // ---- shade every pending lane (shade_kernel, main.cpp:404-425)
+            if (pending) {
+                pending = false;
+                casts++;
+                bool term = true;
+                const int32_t slot = tr.h.slot;
+                if (slot < 0) {
+                    lr = lr + thr * a.env_r;                       // main.cpp:407
+                    lg = lg + thg * a.env_g;
+                    lb = lb + thb * a.env_b;
+                } else {
+                    const float4 m0 = a.sc.snrm[(size_t)slot * 3];
+                    uint32_t mat = f2u(m0.w);
+                    if (kEmit && mat < a.sc.nemit) {
+                        lr = lr + thr * a.sc.emission[mat * 3];
+                        lg = lg + thg * a.sc.emission[mat * 3 + 1];
+                        lb = lb + thb * a.sc.emission[mat * 3 + 2];
+                    }
+                    if (depth + 1 < a.max_depth) {
+                        if (mat >= a.sc.nmat) mat = 0;
+                        thr = thr * a.sc.albedo[mat * 3];            // main.cpp:422
+                        thg = thg * a.sc.albedo[mat * 3 + 1];
+                        thb = thb * a.sc.albedo[mat * 3 + 2];
+                        term = false;
+                        if (depth + 1 >= a.rr_start) {
+                            const float q = fmaxf(thr, fmaxf(thg, thb));
+                            if (q < 1.0f) {
+                                if (rr_uniform(gpix, sample, depth) >= q) {
+                                    term = true;
+                                } else {
+                                    thr = thr / q; thg = thg / q; thb = thb / q;
+                                }
+                            }
+                        }
+                        if (!term) {
+                            const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
+                            const float4 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+                            Pcg32 rng;
+                            rng.state = rs;
+                            rng.inc = ((uint64_t)gpix << 1u) | 1u;
+                            float xi_x, xi_y;
+                            draw2(rng, a.rng_order, xi_x, xi_y);   // main.cpp:413
+                            const float t = tr.h.t, u = tr.h.u, v = tr.h.v;
+                            const float w = (1.0f - u) - v;          // add_math.h:6
+                            const V3 sn = v3((w * m0.x + u * m1.x) + v * m2.x,  // optix_backend.h:483-484
+                                             (w * m0.y + u * m1.y) + v * m2.y,
+                                             (w * m0.z + u * m1.z) + v * m2.z);
+                            const V3 o = tr.o;
+                            const V3 hp = v3(o.x + t * dir.x, o.y + t * dir.y, o.z + t * dir.z);  // :469
+                            const Frame fr = frame_from_normal(sn);  // main.cpp:414
+                            dir = to_world(fr, cosine_hemisphere(xi_x, xi_y));  // main.cpp:418-419, 424
+                            rs = rng.state;
+                            depth++;
+                            tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit);
+                            busy = true;
+                            conts++;
+                        }
+                    }
+                }
+                if (term) {
+                    float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
+                    f[0] = lr;
+                    f[(size_t)a.P] = lg;
+                    f[(size_t)2 * a.P] = lb;
+                }
+            }
+            // ---- new camera paths in free lanes (refill_kernel)
+            uint64_t idle = __ballot(!busy && !pending);
+            while (idle && !(drained && pool == pool_end)) {
+                if (pool == pool_end) {
+                    uint32_t base = 0;
+                    if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, a.chunk);
+                    base = dyn_base + (uint32_t)__shfl((int)base, 0);
+                    if (base >= n) { drained = true; break; }
+                    pool = base;
+                    pool_end = min(base + a.chunk, n);
+                }
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
+                if (!busy && !pending && rank < take) {
+                    const uint64_t wk = a.work0 + pool + rank;
+                    sample = (uint32_t)(wk / a.P);
+                    pix = (uint32_t)(wk - (uint64_t)sample * a.P);
+                    const uint32_t lx = pix % a.W, ly = pix / a.W;
+                    const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
+                    gpix = gy * a.W + lx;                          // main.cpp:379-382
+                    Pcg32 rng;
+                    rng.seed(a.initstate, (uint64_t)gpix);         // main.cpp:376
+                    rng.state = pcg_apply(a.sample_jump[sample], rng.state, rng.inc);
+                    V3 o;
+                    camera_ray(a.cam, rng, a.rng_order, lx, gy, o, dir);
+                    rs = rng.state;
+                    depth = 0;
+                    thr = thg = thb = 1.0f;                        // main.cpp:391
+                    lr = lg = lb = 0.0f;
+                    tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit);
+                    starts++;
+                    busy = true;
+                    if (tr.finished()) {  // empty scene: a miss
+                        busy = false;
+                        pending = true;
+                    }
+                }
+                pool += take;
+                idle = __ballot(!busy && !pending);
+            }
+        }
+        if (!__ballot(busy || pending)) break;
+        if (busy && tr.step(a.sc, stk, st)) {
+            busy = false;
+            pending = true;
+        }
+    }
+    // per-wave sums, one atomic per counter per wave
+#pragma unroll
+    for (uint32_t off = 32; off > 0; off >>= 1) {
+        casts += (uint32_t)__shfl_down((int)casts, off);
+        conts += (uint32_t)__shfl_down((int)conts, off);
+        starts += (uint32_t)__shfl_down((int)starts, off);
+    }
+    if ((threadIdx.x & 63u) == 0) {
+        if (casts) atomicAdd(&a.stats[0], (unsigned long long)casts);
+        if (conts) atomicAdd(&a.stats[1], (unsigned long long)conts);
+        if (starts) atomicAdd(&a.stats[2], (unsigned long long)starts);
+    }
+}
+
 // Per-pixel sum of the per-sample contributions in sample order
 // (film += ... once per sample, main.cpp:407), then film /= spp (main.cpp:429).
 // Chunks of samples carry the running sum in acc.
@@ -681,6 +844,40 @@ hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s) 
     else
         hipLaunchKernelGGL(shade_kernel<false>, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
     return hipGetLastError();
+}
+
+template <typename Tr, bool kEmit>
+static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out) {
+    static thread_local size_t cached_lds = 0;
+    static thread_local uint32_t cached = 0;
+    static thread_local int cached_dev = -1;
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!cached || cached_lds != lds || cached_dev != dev) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_fused_kernel<Tr, kEmit>, kIsectBlock, lds) !=
+                hipSuccess || per_cu <= 0)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        cached = (uint32_t)(per_cu * cus);
+        cached_lds = lds;
+        cached_dev = dev;
+    }
+    const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)cached * a.grid_q8) >> 8)) : cached;
+    const uint32_t blocks = min(scaled, blocks_for(a.count > 0 ? a.count : 1, kIsectBlock));
+    if (lanes_out) *lanes_out = blocks * kIsectBlock;
+    hipLaunchKernelGGL((render_fused_kernel<Tr, kEmit>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out) {
+    if (a.sc.nodes8)
+        return a.sc.emission ? launch_fused_t<Tracer8, true>(a, s, lanes_out)
+                             : launch_fused_t<Tracer8, false>(a, s, lanes_out);
+    return a.sc.emission ? launch_fused_t<Tracer, true>(a, s, lanes_out)
+                         : launch_fused_t<Tracer, false>(a, s, lanes_out);
 }
 
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s) {

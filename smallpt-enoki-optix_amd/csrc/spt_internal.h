@@ -102,6 +102,23 @@ struct RefillArgs {
     bool carry_l;               // write the gathered-radiance planes (emitters present)
 };
 
+// Fused persistent render (one launch per sample chunk): every lane owns a
+// path from camera ray to termination — trace, shade, bounce in registers.
+// Work items [0, count) of the chunk map to w = work0 + i (sample-major).
+struct FusedArgs {
+    DeviceScene sc;
+    Camera cam;
+    const PcgJump* sample_jump;
+    float* sfilm;               // [spp_chunk][3][P]
+    unsigned long long* stats;  // casts, continuations, regenerations
+    uint32_t* next;             // dynamic work counter (zeroed before the launch)
+    uint64_t work0, initstate;
+    uint32_t count, P, W, sample0, max_depth, rr_start, rng_order;
+    uint32_t tile_index, tile_count, rows_per_group;
+    uint32_t refill_idle, static_share_q8, chunk, grid_q8;
+    float env_r, env_g, env_b;
+};
+
 struct HitInfoArgs {
     DeviceScene sc;
     const float *ox, *oy, *oz, *dx, *dy, *dz;
@@ -123,6 +140,7 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
+hipError_t launch_fused(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out);
 hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,

@@ -19,6 +19,8 @@ SPT_RNG_Y_FIRST = 0
 SPT_RNG_X_FIRST = 1
 SPT_FLAG_TIMING = 1
 SPT_FLAG_TRAVERSAL_STATS = 2
+SPT_FLAG_FUSED = 4
+SPT_FLAG_WAVEFRONT = 8
 PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
 
 # Every function include/spt.h declares (the CPU test checks they are exported).

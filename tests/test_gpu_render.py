@@ -65,7 +65,7 @@ def test_render_rng_x_first(gscene, oscene):
 
 @pytest.mark.parametrize("wf", [1, 64, 1000, 48 * 40 * 7, 10**7])
 def test_wavefront_size_invariance(gscene, oscene, wf):
-    got, st = gpu_render(gscene, 48, 40, 7, 4, wavefront_paths=wf)
+    got, st = gpu_render(gscene, 48, 40, 7, 4, wavefront_paths=wf, pipeline="wavefront")
     ref, _ = oracle_render(oscene, 48, 40, 7, 4)
     np.testing.assert_array_equal(got, ref)
     assert st["paths_in_flight"] == min(wf, 48 * 40 * 7)
@@ -219,3 +219,37 @@ def test_city_scene_bitexact():
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts
     assert 0.0 < got.mean() < 1.0
+
+
+@pytest.mark.parametrize("pipeline", ["fused", "wavefront"])
+@pytest.mark.parametrize("w,h,spp,depth,rr", [(64, 48, 4, 4, 99), (40, 30, 6, 6, 2), (33, 17, 3, 1, 99)])
+def test_pipelines_bitexact(mesh, pipeline, w, h, spp, depth, rr):
+    """The fused persistent kernel (trace + shade + new paths in one launch)
+    and the wavefront kernels give the oracle's image bit for bit."""
+    s = sptamd.Scene()
+    s.add_arrays(mesh)
+    s.commit(0)
+    albedo = np.array([[1.0, 1.0, 1.0], [0.8, 0.6, 0.4], [0.9, 0.3, 0.2], [0.2, 0.2, 0.8], [0.9, 0.9, 0.3],
+                       [0.4, 0.4, 0.4]], np.float32)[: len(mesh["kd"])]
+    s.backend.set_albedo(albedo)
+    osc = O.OracleScene(mesh, albedo=albedo)
+    got, st = gpu_render(s, w, h, spp, depth, rr_start_depth=rr, pipeline=pipeline)
+    ref, casts = oracle_render(osc, w, h, spp, depth, rr_start_depth=rr)
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+    assert st["paths"] == w * h * spp
+
+
+def test_fused_emission_and_tiles(cornell):
+    s, osc = cornell
+    kw = dict(camera=scenes.cornell_camera(), rr_start_depth=5, env=(0.0, 0.0, 0.0))
+    got, _ = gpu_render(s, 48, 40, 8, 10, pipeline="fused", **kw)
+    ref, _ = oracle_render(osc, 48, 40, 8, 10, **kw)
+    np.testing.assert_array_equal(got, ref)
+    # a 3-way tile split of the same image, fused
+    img = np.zeros_like(ref)
+    for t in range(3):
+        rows = sptamd.tile_rows(40, t, 3, 4)
+        tile, _ = gpu_render(s, 48, 40, 8, 10, tile_index=t, tile_count=3, rows_per_group=4, pipeline="fused", **kw)
+        img[:, rows, :] = tile
+    np.testing.assert_array_equal(img, ref)
