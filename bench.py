@@ -92,8 +92,8 @@ def cpu_baseline(mesh, args, threads, kw, albedo, emission):
 
     sc = O.OracleScene(mesh, albedo=albedo, emission=emission)
     p = O.reference_params(args.width, args.height, args.spp, args.depth, **kw)
-    stride = 64
-    rows = np.arange(0, args.height, stride, dtype=np.int32)[:4]
+    # calibrate on 8 rows spread over the image (sky rows at the top are cheap)
+    rows = np.unique(np.linspace(0, args.height - 1, 8).astype(np.int32))
     t0 = time.perf_counter()
     sc.render(p, rows=rows, nthreads=threads)
     dt = time.perf_counter() - t0
@@ -206,7 +206,7 @@ def main():
         bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic, traffic_src = None, None
-        if os.path.exists(TRAFFIC_JSON):  # FETCH_SIZE/WRITE_SIZE passes of this command (profiles/)
+        if args.config == 1 and os.path.exists(TRAFFIC_JSON):  # FETCH_SIZE/WRITE_SIZE passes (profiles/)
             tj = json.load(open(TRAFFIC_JSON))
             traffic, traffic_src = round(tj["traffic_bytes_per_launch"]), tj["source"][0].rsplit("/", 1)[0]
         rec = {
