@@ -27,6 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "isect_traffic.json")  # tools/pmc_traffic.py output
 ISECT_BYTES_PER_CAST = 44      # ray 24 B + meta 4 B in, hit 16 B out
+FUSED_BYTES_PER_PATH = 12      # per-sample film RGB write
 
 
 # BASELINE.json configs (index = position in "configs"); 1 is the headline.
@@ -53,9 +54,12 @@ def parse():
     ap.add_argument("--scene", default="")
     ap.add_argument("--rows-per-group", type=int, default=8)
     ap.add_argument("--wavefront", type=int, default=0, help="paths in flight per launch (0 = auto)")
-    ap.add_argument("--pipeline", choices=["wavefront", "fused"], default="wavefront",
-                    help="isect/shade/refill kernels over path queues (north-star design) or one fused "
-                         "persistent trace+shade kernel")
+    ap.add_argument("--pipeline", choices=["auto", "wavefront", "fused"], default="auto",
+                    help="isect/shade/refill kernels over path queues (north-star design), one fused "
+                         "persistent trace+shade kernel, or auto (the library picks by per-GPU job size: "
+                         "fused for at most two wavefronts of paths)")
+    ap.add_argument("--timing-all", action="store_true",
+                    help="HIP events around every launch (shade/refill/resolve ms too; costs ~5%% host time)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -158,7 +162,9 @@ def main():
     W, H = args.width, args.height
     R = args.rows_per_group
     params = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
-                                wavefront_paths=args.wavefront, timing=True, pipeline=args.pipeline, **kw)
+                                wavefront_paths=args.wavefront,
+                                timing="all" if args.timing_all else True,
+                                pipeline=None if args.pipeline == "auto" else args.pipeline, **kw)
     dev = torch.device("cuda", local)
     tg = TileGather(H, W, rank, world, R, dev)
     film = tg.tile_view()
@@ -200,13 +206,20 @@ def main():
     paths = W * H * args.spp * args.steps
     value = paths / elapsed / 1e6
     if rank == 0:
-        # isect roofline: algorithmic bytes per launch / average launch time (rank 0's tile)
+        # roofline of the dominant kernel: algorithmic bytes per launch / average
+        # launch time (HIP events, rank 0's tile).  Wavefront: isect_queue_kernel,
+        # 44 B per ray cast.  Fused: render_fused_kernel, whose only HBM stream is
+        # the per-sample film write (12 B per path; rays stay in registers).
+        fused = bool(st.get("fused"))
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
-        bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
+        if fused:
+            bytes_per_launch = st["paths"] * args.steps / launches * FUSED_BYTES_PER_PATH
+        else:
+            bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic, traffic_src = None, None
-        if args.config == 1 and os.path.exists(TRAFFIC_JSON):  # FETCH_SIZE/WRITE_SIZE passes (profiles/)
+        if args.config == 1 and not fused and world == 1 and os.path.exists(TRAFFIC_JSON):  # PMC passes (profiles/)
             tj = json.load(open(TRAFFIC_JSON))
             traffic, traffic_src = round(tj["traffic_bytes_per_launch"]), tj["source"][0].rsplit("/", 1)[0]
         rec = {
@@ -223,7 +236,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
-            "config": {"pipeline": args.pipeline,
+            "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
                        "workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
@@ -232,12 +245,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "isect_queue_kernel" if args.pipeline == "wavefront" else "render_fused_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "kernel": "render_fused_kernel" if fused else "isect_queue_kernel", "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
                          "grays_per_s": round(agg["ray_casts"] / (agg["isect_ms"] * 1e-3) / 1e9, 4)
                          if agg["isect_ms"] else None},
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
-                                   ("isect_ms", "shade_ms", "camera_ms", "resolve_ms")},
+                                   (("isect_ms", "shade_ms", "camera_ms", "resolve_ms") if args.timing_all
+                                    else ("isect_ms",))},
             "bvh": dict({k: sstats[k] for k in ("nodes", "max_depth", "build_ms", "sah_cost", "device_bytes")},
                         commit_s=round(t_commit, 3)),
         }

@@ -75,10 +75,13 @@ enum {
 };
 
 enum {
-    SPT_FLAG_TIMING = 1u,          /* record HIP events around every isect/shade launch */
+    SPT_FLAG_TIMING = 1u,          /* record HIP events around every isect launch (isect_ms) */
     SPT_FLAG_TRAVERSAL_STATS = 2u, /* count node visits / triangle tests (slower variant; wavefront) */
     SPT_FLAG_FUSED = 4u,           /* one persistent trace+shade kernel per sample chunk */
-    SPT_FLAG_WAVEFRONT = 8u        /* isect / shade / refill kernels over path queues */
+    SPT_FLAG_WAVEFRONT = 8u,       /* isect / shade / refill kernels over path queues
+                                      (neither flag: env SPT_FUSED, else fused iff the job
+                                      is at most two wavefronts of paths) */
+    SPT_FLAG_TIMING_ALL = 16u      /* with SPT_FLAG_TIMING: also shade / refill / resolve launches */
 };
 
 /* The render loop of main.cpp:354-429 plus the tile/wavefront knobs. */
@@ -106,7 +109,7 @@ typedef struct spt_render_stats {
     uint64_t iterations;        /* isect+shade+refill rounds (each over every sub-wavefront) */
     uint32_t paths_in_flight;   /* wavefront capacity (queue slots) */
     uint32_t tile_rows;
-    double isect_ms, shade_ms, camera_ms, resolve_ms; /* SPT_FLAG_TIMING only (camera = refills) */
+    double isect_ms, shade_ms, camera_ms, resolve_ms; /* isect: SPT_FLAG_TIMING; others: + SPT_FLAG_TIMING_ALL (camera = refills) */
     double total_ms;            /* host wall time of the call (includes final sync) */
     uint64_t isect_nodes;       /* SPT_FLAG_TRAVERSAL_STATS: inner nodes visited (all lanes) */
     uint64_t isect_tris;        /*   triangle tests */
@@ -114,7 +117,7 @@ typedef struct spt_render_stats {
     uint64_t isect_wave_steps;  /*   traversal loop iterations summed over waves */
     uint64_t isect_launches;    /* SPT_FLAG_TIMING: isect launches timed (all streams) */
     uint32_t streams;           /* sub-wavefronts (HIP streams) used, env SPT_STREAMS */
-    uint32_t reserved;
+    uint32_t fused;             /* 1: the fused pipeline ran, 0: the wavefront */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

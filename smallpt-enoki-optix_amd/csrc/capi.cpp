@@ -111,7 +111,7 @@ struct Sub {
     char* hits = nullptr;
     Counters* cnt = nullptr;
     hipStream_t stream = nullptr;       // internal stream (sub 0 runs on the caller's)
-    uint32_t* host_counts = nullptr;    // pinned, 2 slots
+    Counters* host_cnt = nullptr;       // pinned, 2 slots (counter snapshots read one batch behind)
     hipEvent_t count_ev[2] = {nullptr, nullptr};
     hipEvent_t join_ev = nullptr;
 };
@@ -123,20 +123,18 @@ struct Workspace {
     PcgJump* jumps = nullptr;
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
     Stats* stats = nullptr;
-    uint64_t* host_cursor = nullptr;    // pinned, kMaxStreams slots
     hipEvent_t fork_ev = nullptr;
     std::vector<hipEvent_t> events;
 
     void release() {
         for (Sub& b : sub) {
             hfree(b.qa); hfree(b.qb); hfree(b.hits); hfree(b.cnt);
-            if (b.host_counts) (void)hipHostFree(b.host_counts);
+            if (b.host_cnt) (void)hipHostFree(b.host_cnt);
             for (auto& e : b.count_ev) if (e) (void)hipEventDestroy(e);
             if (b.join_ev) (void)hipEventDestroy(b.join_ev);
             if (b.stream) (void)hipStreamDestroy(b.stream);
         }
         hfree(film); hfree(jumps); hfree(stats);
-        if (host_cursor) (void)hipHostFree(host_cursor);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         for (auto e : events) (void)hipEventDestroy(e);
         *this = Workspace();
@@ -227,7 +225,7 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, size_t film_flo
             b.cap = cap;
         }
         if (!b.cnt) HIP_TRY(hipMalloc((void**)&b.cnt, sizeof(Counters)));
-        if (!b.host_counts) HIP_TRY(hipHostMalloc((void**)&b.host_counts, 16, hipHostMallocDefault));
+        if (!b.host_cnt) HIP_TRY(hipHostMalloc((void**)&b.host_cnt, 2 * sizeof(Counters), hipHostMallocDefault));
         for (auto& e : b.count_ev)
             if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (!b.join_ev) HIP_TRY(hipEventCreateWithFlags(&b.join_ev, hipEventDisableTiming));
@@ -247,8 +245,6 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, size_t film_flo
         ws.jump_cap = njumps;
     }
     if (!ws.stats) HIP_TRY(hipMalloc((void**)&ws.stats, sizeof(Stats)));
-    if (!ws.host_cursor) HIP_TRY(hipHostMalloc((void**)&ws.host_cursor, sizeof(uint64_t) * kMaxStreams,
-                                              hipHostMallocDefault));
     if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
     return SPT_OK;
 }
@@ -542,24 +538,32 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     }
     if (!film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
 
-    // Pipeline: the wavefront (isect / shade / refill over path queues, the
-    // north-star design) or the fused persistent kernel.  Traversal counters
-    // exist in the wavefront isect kernel only.
-    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
-    bool fused = env_u32("SPT_FUSED", 0, 0, 1) != 0;
-    if (p.flags & SPT_FLAG_FUSED) fused = true;
-    if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
-
     // Wavefront capacity.  Each isect launch ends in a tail where its last rays
     // finish while most lanes idle; 8M paths in flight (~1 GB of queues)
     // amortise it (measured: 1M 913, 2M 1191, 8M 1792 Mpaths/s on MI355X).
     uint64_t C = p.wavefront_paths ? p.wavefront_paths : (1ull << 23);
+
+    // Pipeline: the wavefront (isect / shade / refill over path queues, the
+    // north-star design) or the fused persistent kernel (bit-identical).  The
+    // flags choose; else env SPT_FUSED=0/1; else by job size: a job of at most
+    // two wavefronts is mostly per-cast launch tails on the wavefront (queues
+    // shrink cast by cast with no work left to refill them), where the fused
+    // kernel's single tail wins — e.g. one rank's 1/8 of the headline image:
+    // fused 2308 vs wavefront 1982 Mpaths/s; whole image: 2353 vs 2825.
+    // Traversal counters exist in the wavefront isect kernel only.
+    const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
+    const uint32_t fused_env = env_u32("SPT_FUSED", 2, 0, 2);
+    bool fused = fused_env == 2 ? P * p.spp <= 2 * C : fused_env == 1;
+    if (p.flags & SPT_FLAG_FUSED) fused = true;
+    if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);
     // The wavefront is split into K sub-wavefronts on their own streams, so one
     // sub-wavefront's launch tail overlaps the others' work.
-    int K = fused ? 1 : (int)env_u32("SPT_STREAMS", 2, 1, kMaxStreams);
+    // Measured on the headline config: 1 stream 1982, 2: 2649, 3: 2769, 4: 2791 Mpaths/s
+    // (4 = the box's hardware queues per process, GPU_MAX_HW_QUEUES).
+    int K = fused ? 1 : (int)env_u32("SPT_STREAMS", 4, 1, kMaxStreams);
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
@@ -570,7 +574,10 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     spt_status st = ensure_workspace(sc->ws, K, Ck, (size_t)chunk * 3 * P + 3 * P, p.spp);
     if (st) return st;
     Workspace& ws = sc->ws;
+    // HIP events around the isect launches (the roofline kernel); every other
+    // launch only with SPT_FLAG_TIMING_ALL (each event pair costs host time).
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
+    const bool timing_all = timing && (p.flags & SPT_FLAG_TIMING_ALL) != 0;
 
     // PCG32 jump to each sample's first draw: s * (4 + 2D) (main.cpp:395,396,413).
     const uint64_t per_sample = 4ull + 2ull * p.max_depth;
@@ -594,12 +601,13 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     auto mark = [&](int kind, hipStream_t sk, auto&& launch) -> spt_status {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         spt_status s2;
-        if (timing) {
+        const bool tm = kind == 1 ? timing : timing_all;
+        if (tm) {
             if ((s2 = get_event(ws, ev, &e0)) || (s2 = get_event(ws, ev + 1, &e1))) return s2;
             HIP_TRY(hipEventRecord(e0, sk));
         }
         HIP_TRY(launch());
-        if (timing) {
+        if (tm) {
             HIP_TRY(hipEventRecord(e1, sk));
             timed.push_back({ev, kind});
             ev += 2;
@@ -689,42 +697,59 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         // fork: the sub-wavefront streams start after everything queued so far
         HIP_TRY(hipEventRecord(ws.fork_ev, stream));
         for (int k = 1; k < K; k++) HIP_TRY(hipStreamWaitEvent(strm[k], ws.fork_ev, 0));
+        uint64_t started[kMaxStreams], sub_end[kMaxStreams];  // work items known started; end of the share
         for (int k = 0; k < K; k++) {
             Sub& b = ws.sub[k];
             // contiguous share of the chunk's work items (sample-major)
             const uint64_t wb = w0 + L * k / K, we = w0 + L * (k + 1) / K;
             HIP_TRY(hipMemsetAsync(b.cnt, 0, sizeof(Counters), strm[k]));
-            // Pinned source, read when the copy executes: every earlier copy has
-            // completed (the previous chunk synchronised on later events).
-            ws.host_cursor[k] = wb;
-            HIP_TRY(hipMemcpyAsync(&b.cnt->cursor[1], &ws.host_cursor[k], sizeof(uint64_t), hipMemcpyHostToDevice,
-                                   strm[k]));
             ra[k].work_end = we;
             sa[k].sample0 = s0;
-            ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = &b.cnt->cursor[1];
+            // the first refill starts at the sub-wavefront's first work item
+            ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = nullptr; ra[k].cursor_init = wb;
             ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];
-            if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], (uint32_t)b.cap, strm[k]); }))) return st;
+            ra[k].surv_clear = nullptr;
+            const uint32_t first = (uint32_t)std::min<uint64_t>(b.cap, we - wb);
+            sub_end[k] = we;
+            started[k] = wb + first;
+            if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], first, strm[k]); }))) return st;
         }
         // isect -> shade -> refill per sub-wavefront until every queue drains.
-        // Live counts are read back once per batch, one batch behind the
-        // launches; they never grow, so a stale value is a safe grid size.
+        // A path cast in iteration i was started by the refill after iteration
+        // <= i - 1 and makes at most max_depth casts, so once every work item
+        // has been started (the cursor, read back one batch behind the
+        // launches, reached the end) the queue is empty max_depth iterations
+        // later: the loop stops there without a further readback.  Live counts
+        // never grow after that, so a stale count is a safe grid size, and a
+        // refill's grid is bounded by the work not yet known to be started.
         const uint64_t max_iters = (L * p.max_depth + Ck - 1) / Ck + p.max_depth + 64;
         uint32_t known[kMaxStreams];
-        int cur[kMaxStreams], pending[kMaxStreams];
+        int cur[kMaxStreams], pending[kMaxStreams], pend_cur[kMaxStreams];
+        uint64_t pend_it[kMaxStreams], limit[kMaxStreams];
         bool live[kMaxStreams];
         for (int k = 0; k < K; k++) {
-            known[k] = (uint32_t)ws.sub[k].cap;
+            known[k] = (uint32_t)std::min<uint64_t>(ws.sub[k].cap, started[k] - (w0 + L * k / K));
             cur[k] = 0;
             pending[k] = -1;
-            live[k] = true;
+            pend_cur[k] = 0;
+            pend_it[k] = 0;
+            // everything fit in the first refill: exactly max_depth iterations
+            limit[k] = started[k] >= sub_end[k] ? p.max_depth : UINT64_MAX;
+            live[k] = known[k] > 0;
         }
         uint64_t it = 0;
         uint32_t batch = 4, nbatch = 0;
-        int nlive = K;
+        int nlive = 0;
+        for (int k = 0; k < K; k++) nlive += live[k] ? 1 : 0;
         while (nlive > 0) {
-            for (uint32_t bi = 0; bi < batch; bi++) {
+            for (uint32_t bi = 0; bi < batch && nlive > 0; bi++) {
                 for (int k = 0; k < K; k++) {
                     if (!live[k]) continue;
+                    if (it >= limit[k]) {  // drained by construction
+                        live[k] = false;
+                        nlive--;
+                        continue;
+                    }
                     Sub& b = ws.sub[k];
                     const int c = cur[k], nx = 1 - c;
                     ia[k].q = q[k][c];
@@ -734,40 +759,49 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
                                                : launch_isect_queue(ia[k], known[k], strm[k]);
                          })))
                         return st;
-                    HIP_TRY(hipMemsetAsync(&b.cnt->surv[nx], 0, sizeof(uint32_t), strm[k]));
+                    // surv[nx] was zeroed by the previous refill (surv_clear)
                     sa[k].in = q[k][c]; sa[k].out = q[k][nx];
                     sa[k].count_in = &b.cnt->qn[c];
                     sa[k].count_out = &b.cnt->surv[nx];
                     if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], known[k], strm[k]); }))) return st;
                     ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
                     ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
-                    if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], (uint32_t)b.cap, strm[k]); })))
+                    ra[k].surv_clear = &b.cnt->surv[c];
+                    // new paths: at most the work not yet known to be started (one
+                    // block still runs to carry the counters over)
+                    const uint32_t fill = (uint32_t)std::min<uint64_t>(b.cap, sub_end[k] - started[k]);
+                    if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], fill, strm[k]); })))
                         return st;
                     cur[k] = nx;
                 }
                 it++;
             }
+            if (nlive == 0) break;
             const int slot = (int)(nbatch++ & 1u);
             for (int k = 0; k < K; k++) {
-                if (!live[k]) continue;
+                if (!live[k] || limit[k] != UINT64_MAX) continue;  // bounded streams need no readback
                 Sub& b = ws.sub[k];
-                HIP_TRY(hipMemcpyAsync(b.host_counts + slot, &b.cnt->qn[cur[k]], sizeof(uint32_t),
-                                       hipMemcpyDeviceToHost, strm[k]));
+                HIP_TRY(hipMemcpyAsync(b.host_cnt + slot, b.cnt, sizeof(Counters), hipMemcpyDeviceToHost, strm[k]));
                 HIP_TRY(hipEventRecord(b.count_ev[slot], strm[k]));
             }
             for (int k = 0; k < K; k++) {
-                if (!live[k]) continue;
+                if (!live[k] || limit[k] != UINT64_MAX) continue;
                 Sub& b = ws.sub[k];
                 if (pending[k] >= 0) {
                     HIP_TRY(hipEventSynchronize(b.count_ev[pending[k]]));
-                    known[k] = b.host_counts[pending[k]];
+                    const Counters& hc = b.host_cnt[pending[k]];
+                    known[k] = hc.qn[pend_cur[k]];
+                    started[k] = std::max<uint64_t>(started[k], hc.cursor[pend_cur[k]]);
                     if (known[k] == 0) {
                         live[k] = false;
                         nlive--;
                         continue;
                     }
+                    if (started[k] >= sub_end[k]) limit[k] = pend_it[k] + p.max_depth;
                 }
                 pending[k] = slot;
+                pend_cur[k] = cur[k];
+                pend_it[k] = it;
             }
             if (it > max_iters)
                 return fail(SPT_ERR_HIP, "spt_render: queue did not drain after %llu iterations",
@@ -810,6 +844,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         rs.isect_launches = nis;
     }
     rs.streams = (uint32_t)K;
+    rs.fused = fused ? 1u : 0u;
     rs.total_ms = now_ms() - wall0;
     if (stats_out) *stats_out = rs;
     return SPT_OK;

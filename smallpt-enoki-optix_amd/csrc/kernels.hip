@@ -396,7 +396,7 @@ __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o,
 // sample's first draw, s * (4 + 2D) draws (main.cpp:395,396,413 per sample).
 __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     const uint32_t surv = *a.surv;
-    const uint64_t cur = *a.cursor_in;
+    const uint64_t cur = a.cursor_in ? *a.cursor_in : a.cursor_init;
     const uint64_t avail = a.work_end > cur ? a.work_end - cur : 0;
     const uint32_t room = a.capacity - surv;
     const uint32_t total = (uint32_t)(avail < room ? avail : room);
@@ -405,6 +405,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         *a.cursor_out = cur + total;
         *a.qn_out = surv + total;
         *a.isect_next = 0;
+        if (a.surv_clear) *a.surv_clear = 0;
         if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
     }
     if (i >= total) return;

@@ -89,10 +89,12 @@ struct RefillArgs {
     PathQueue q;
     Camera cam;
     const uint32_t* surv;       // survivors already in the queue
-    const uint64_t* cursor_in;
+    const uint64_t* cursor_in;  // null: start at cursor_init (the first refill of a chunk)
+    uint64_t cursor_init;
     uint64_t* cursor_out;       // written by thread 0 only
     uint32_t* qn_out;           // queue count for the next isect, thread 0 only
     uint32_t* isect_next;       // zeroed by thread 0 for the next isect launch
+    uint32_t* surv_clear;       // zeroed by thread 0: the next shade's survivor counter (may be null)
     const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
     unsigned long long* stats;
     uint64_t work_end;          // W_total (work items of this chunk end here)

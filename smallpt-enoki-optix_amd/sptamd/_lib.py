@@ -21,6 +21,7 @@ SPT_FLAG_TIMING = 1
 SPT_FLAG_TRAVERSAL_STATS = 2
 SPT_FLAG_FUSED = 4
 SPT_FLAG_WAVEFRONT = 8
+SPT_FLAG_TIMING_ALL = 16
 PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
 
 # Every function include/spt.h declares (the CPU test checks they are exported).
@@ -76,7 +77,7 @@ class RenderStats(ctypes.Structure):
                 ("resolve_ms", c_double), ("total_ms", c_double),
                 ("isect_nodes", c_uint64), ("isect_tris", c_uint64), ("isect_lane_steps", c_uint64),
                 ("isect_wave_steps", c_uint64), ("isect_launches", c_uint64), ("streams", c_uint32),
-                ("reserved", c_uint32)]
+                ("fused", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

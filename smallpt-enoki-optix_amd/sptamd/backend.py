@@ -200,9 +200,10 @@ def reference_camera() -> dict:
 
 def make_params(width: int, height: int, spp: int, max_depth: int, camera: Optional[dict] = None,
                 tile_index: int = 0, tile_count: int = 1, rows_per_group: int = 1, wavefront_paths: int = 0,
-                rr_start_depth: int = 1, rng_order: int = 0, env=(1.0, 1.0, 1.0), timing: bool = False,
+                rr_start_depth: int = 1, rng_order: int = 0, env=(1.0, 1.0, 1.0), timing=False,
                 rng_initstate: int = _lib.PCG32_DEFAULT_STATE, pipeline: Optional[str] = None) -> RenderParams:
-    """pipeline: None (library default / SPT_FUSED), "wavefront" or "fused"."""
+    """pipeline: None (library default / SPT_FUSED), "wavefront" or "fused".
+    timing: False, True (HIP events around isect launches) or "all" (every launch)."""
     p = _lib.default_params()
     p.width, p.height, p.spp, p.max_depth = width, height, spp, max_depth
     cam = reference_camera() if camera is None else camera
@@ -218,7 +219,9 @@ def make_params(width: int, height: int, spp: int, max_depth: int, camera: Optio
     p.rng_order = rng_order
     p.rng_initstate = rng_initstate
     p.env[:] = [float(e) for e in env]
-    p.flags = _lib.SPT_FLAG_TIMING if timing else 0
+    p.flags = _lib.SPT_FLAG_TIMING if timing else 0     # timing="all": every launch, not only isect
+    if timing == "all":
+        p.flags |= _lib.SPT_FLAG_TIMING_ALL
     if pipeline == "fused":
         p.flags |= _lib.SPT_FLAG_FUSED
     elif pipeline == "wavefront":

@@ -35,9 +35,17 @@ def oscene(mesh):
 
 
 def gpu_render(gscene, w, h, spp, depth, **kw):
+    """Without an explicit pipeline: render with both (wavefront and fused),
+    require identical films, return the wavefront's."""
+    if "pipeline" not in kw:
+        got, st = gpu_render(gscene, w, h, spp, depth, pipeline="wavefront", **kw)
+        fused, _ = gpu_render(gscene, w, h, spp, depth, pipeline="fused", **kw)
+        np.testing.assert_array_equal(fused, got)
+        return got, st
     p = sptamd.make_params(w, h, spp, depth, **kw)
     film, st = gscene.render(p)
     torch.cuda.synchronize()
+    assert st["fused"] == (kw["pipeline"] == "fused")
     return film.cpu().numpy(), st
 
 

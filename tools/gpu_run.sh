@@ -37,6 +37,9 @@ for s in "$@"; do
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
+    tilesim) run tilesim 400 python tools/tile_sim.py ;;
+    tilesimt) run tilesimt 400 python tools/tile_sim.py --timing ;;
+    tilesimf) run tilesimf 400 python tools/tile_sim.py --pipeline fused ;;
     listctr) run listctr 300 rocprofv3 -L ;;
     pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD --kernel-include-regex isect_queue -d gpurun_out/pmc_sq -o run --output-format csv -- python tools/trav_stats.py --depths 8 --spp 8 ;;
     pmctcc) run pmctcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum --kernel-include-regex isect_queue -d gpurun_out/pmc_tcc -o run --output-format csv -- python tools/trav_stats.py --depths 8 --spp 8 ;;

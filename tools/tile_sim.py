@@ -1,0 +1,69 @@
+"""Strong-scaling projection on one GPU: render tile 0 of N (the share one
+rank gets under `bench.py --gpus N`) and report the tile's Mpaths/s and the
+projected whole-job rate N x that (ignores the gather, ~0.2 ms).
+
+    python tools/tile_sim.py [--config 1] [--tiles 1 2 4 8] [--steps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--tiles", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--rows-per-group", type=int, default=8)
+    ap.add_argument("--pipeline", default="wavefront")
+    ap.add_argument("--timing", action="store_true", help="HIP events around every launch (as bench.py)")
+    args = ap.parse_args()
+    import torch
+
+    import bench
+    import sptamd
+    from sptamd import scenes
+
+    cfg = bench.CONFIGS[args.config]
+    ns = argparse.Namespace(scene=cfg["scene"], smallpt=cfg["smallpt"])
+    src, kw, alb, _ = bench.workload(ns, scenes)
+    scene = sptamd.Scene()
+    if isinstance(src, str):
+        scene.add_triangle_mesh(src)
+    else:
+        scene.add_arrays(src)
+    scene.commit(0)
+    if alb:
+        a, e = scenes.smallpt_materials(scene.mesh)
+        scene.backend.set_albedo(a)
+        scene.backend.set_emission(e)
+    W, H, spp, D = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
+    for n in args.tiles:
+        p = sptamd.make_params(W, H, spp, D, tile_index=0, tile_count=n, rows_per_group=args.rows_per_group,
+                               timing=args.timing, pipeline=args.pipeline, **kw)
+        rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
+        film = torch.empty((3, rows, W), dtype=torch.float32, device="cuda")
+        scene.render(p, film=film)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            _, st = scene.render(p, film=film)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        paths = rows * W * spp
+        rate = paths / dt / 1e6
+        print(json.dumps({"tiles": n, "tile_rows": rows, "ms_per_step": round(dt * 1e3, 3),
+                          "tile_mpaths_s": round(rate, 1), "projected_job_mpaths_s": round(rate * n, 1),
+                          "iterations": st["iterations"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
