@@ -103,14 +103,13 @@ def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     dt = time.perf_counter() - t0
     # scale the sample to ~cpu_baseline_seconds of work, rows spread over the image
     want = int(max(1, min(args.height, len(rows) * args.cpu_baseline_seconds / max(dt, 1e-3))))
-    stride = max(1, args.height // want)
-    rows = np.arange(0, args.height, stride, dtype=np.int32)[:want]
+    rows = np.unique(np.linspace(0, args.height - 1, want).astype(np.int32))
     t0 = time.perf_counter()
     _, casts = sc.render(p, rows=rows, nthreads=threads)
     dt = time.perf_counter() - t0
     paths = rows.size * args.width * args.spp
     return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"{rows.size} of {args.height} rows (every {stride}th) x {args.width} px x {args.spp} spp, "
+            "sample": f"{rows.size} of {args.height} rows (evenly spaced) x {args.width} px x {args.spp} spp, "
                       f"depth {args.depth}: {paths} paths, {casts} casts in {dt:.2f} s "
                       f"(oracle: C restatement, median-split BVH, {threads} threads)"}
 
@@ -183,7 +182,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
-           "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0}
+           "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0}
     st = {}
     for _ in range(args.steps):
         st = step()
@@ -210,14 +209,22 @@ def main():
         # launch time (HIP events, rank 0's tile).  Wavefront: isect_queue_kernel,
         # 44 B per ray cast.  Fused: render_fused_kernel, whose only HBM stream is
         # the per-sample film write (12 B per path; rays stay in registers).
+        # The wavefront runs K sub-wavefronts on K streams, so isect launches
+        # overlap: `achieved` divides the bytes of all launches by the union of
+        # their intervals (the time the isect kernel occupies the chip), and
+        # `per_launch` is bytes per launch / average launch duration (the
+        # figure rocprofv3's per-kernel average reproduces).
         fused = bool(st.get("fused"))
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
         if fused:
-            bytes_per_launch = st["paths"] * args.steps / launches * FUSED_BYTES_PER_PATH
+            total_bytes = st["paths"] * args.steps * FUSED_BYTES_PER_PATH
         else:
-            bytes_per_launch = agg["ray_casts"] / launches * ISECT_BYTES_PER_CAST
-        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+            total_bytes = agg["ray_casts"] * ISECT_BYTES_PER_CAST
+        bytes_per_launch = total_bytes / launches
+        busy_ms = agg["isect_busy_ms"]
+        achieved = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+        per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic, traffic_src = None, None
         if args.config == 1 and not fused and world == 1 and os.path.exists(TRAFFIC_JSON):  # PMC passes (profiles/)
             tj = json.load(open(TRAFFIC_JSON))
@@ -245,10 +252,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "render_fused_kernel" if fused else "isect_queue_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",
+                         "launches_per_step": round(launches / args.steps, 2),
+                         "busy_ms_per_step": round(busy_ms / args.steps, 4),
+                         "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                         "grays_per_s": round(agg["ray_casts"] / (agg["isect_ms"] * 1e-3) / 1e9, 4)
-                         if agg["isect_ms"] else None},
+                         "per_launch": {"achieved": round(per_launch, 2), "frac": round(per_launch / HBM_PEAK_GBS, 5)},
+                         "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None},
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
                                    (("isect_ms", "shade_ms", "camera_ms", "resolve_ms") if args.timing_all
                                     else ("isect_ms",))},

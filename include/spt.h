@@ -118,6 +118,8 @@ typedef struct spt_render_stats {
     uint64_t isect_launches;    /* SPT_FLAG_TIMING: isect launches timed (all streams) */
     uint32_t streams;           /* sub-wavefronts (HIP streams) used, env SPT_STREAMS */
     uint32_t fused;             /* 1: the fused pipeline ran, 0: the wavefront */
+    double isect_busy_ms;       /* SPT_FLAG_TIMING: union of the isect launch intervals
+                                   (launches on the K streams overlap; isect_ms sums them) */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

@@ -595,9 +595,15 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
     HIP_TRY(hipMemsetAsync(ws.stats, 0, sizeof(Stats), stream));
+    // time origin for the isect launch intervals (their union = isect busy time)
+    hipEvent_t origin_ev = nullptr;
+    if (timing) {
+        if ((st = get_event(ws, 0, &origin_ev))) return st;
+        HIP_TRY(hipEventRecord(origin_ev, stream));
+    }
 
     std::vector<std::pair<size_t, int>> timed;  // (start event index, 0 refill 1 isect 2 shade 3 resolve)
-    size_t ev = 0;
+    size_t ev = 1;  // events[0] is the origin
     auto mark = [&](int kind, hipStream_t sk, auto&& launch) -> spt_status {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         spt_status s2;
@@ -833,15 +839,34 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     rs.isect_wave_steps = hstats[6];
     if (timing) {
         uint64_t nis = 0;
+        std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin
         for (auto& tk : timed) {
             float ms = 0.0f;
             HIP_TRY(hipEventElapsedTime(&ms, ws.events[tk.first], ws.events[tk.first + 1]));
             if (tk.second == 0) rs.camera_ms += ms;
-            else if (tk.second == 1) { rs.isect_ms += ms; nis++; }
-            else if (tk.second == 2) rs.shade_ms += ms;
+            else if (tk.second == 1) {
+                rs.isect_ms += ms;
+                nis++;
+                float t0 = 0.0f;
+                HIP_TRY(hipEventElapsedTime(&t0, origin_ev, ws.events[tk.first]));
+                iv.push_back({t0, t0 + ms});
+            } else if (tk.second == 2) rs.shade_ms += ms;
             else rs.resolve_ms += ms;
         }
         rs.isect_launches = nis;
+        // launches on the K streams overlap: busy time = union of their intervals
+        std::sort(iv.begin(), iv.end());
+        float lo = 0.0f, hi = -1.0f;
+        for (auto& x : iv) {
+            if (x.first > hi) {
+                if (hi > lo) rs.isect_busy_ms += hi - lo;
+                lo = x.first;
+                hi = x.second;
+            } else {
+                hi = std::max(hi, x.second);
+            }
+        }
+        if (hi > lo) rs.isect_busy_ms += hi - lo;
     }
     rs.streams = (uint32_t)K;
     rs.fused = fused ? 1u : 0u;

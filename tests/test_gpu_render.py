@@ -45,7 +45,8 @@ def gpu_render(gscene, w, h, spp, depth, **kw):
     p = sptamd.make_params(w, h, spp, depth, **kw)
     film, st = gscene.render(p)
     torch.cuda.synchronize()
-    assert st["fused"] == (kw["pipeline"] == "fused")
+    if st["paths"]:  # an empty tile returns before choosing a pipeline
+        assert st["fused"] == (kw["pipeline"] == "fused")
     return film.cpu().numpy(), st
 
 

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--tiles", type=int, nargs="+", default=[1, 2, 4, 8])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rows-per-group", type=int, default=8)
-    ap.add_argument("--pipeline", default="wavefront")
+    ap.add_argument("--pipeline", default=None, help="wavefront | fused (default: the library's auto choice)")
     ap.add_argument("--timing", action="store_true", help="HIP events around every launch (as bench.py)")
     args = ap.parse_args()
     import torch
@@ -62,7 +62,7 @@ def main():
         rate = paths / dt / 1e6
         print(json.dumps({"tiles": n, "tile_rows": rows, "ms_per_step": round(dt * 1e3, 3),
                           "tile_mpaths_s": round(rate, 1), "projected_job_mpaths_s": round(rate * n, 1),
-                          "iterations": st["iterations"]}), flush=True)
+                          "iterations": st["iterations"], "fused": st["fused"]}), flush=True)
 
 
 if __name__ == "__main__":
