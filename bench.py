@@ -262,7 +262,7 @@ def main():
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
                                    (("isect_ms", "shade_ms", "camera_ms", "resolve_ms") if args.timing_all
                                     else ("isect_ms",))},
-            "bvh": dict({k: sstats[k] for k in ("nodes", "max_depth", "build_ms", "sah_cost", "device_bytes")},
+            "bvh": dict({k: sstats[k] for k in ("builder", "nodes", "max_depth", "build_ms", "sah_cost", "device_bytes")},
                         commit_s=round(t_commit, 3)),
         }
         if args.save:

@@ -127,9 +127,9 @@ typedef struct spt_scene_stats {
     uint32_t max_depth;         /* BVH depth (sets the LDS stack depth) */
     uint32_t max_leaf;
     uint32_t bvh_width;         /* 8: compressed 8-wide BVH (default), 2: BVH2 (env SPT_BVH=2) */
-    uint32_t reserved;
+    uint32_t builder;           /* SPT_BUILD_HOST_SAH or SPT_BUILD_GPU_PLOC: the build that ran */
     uint64_t device_bytes;
-    double build_ms;            /* host SAH build */
+    double build_ms;            /* BVH build (host SAH, or GPU PLOC + collapse, synchronised) */
     double sah_cost;
 } spt_scene_stats;
 
@@ -160,6 +160,21 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
                             const int32_t* nrm_tri, const float* nrm, uint64_t nnrm,
                             const int32_t* tc_tri, const float* tc, uint64_t ntc,
                             const int32_t* mat_id, spt_scene* out);
+
+/* Acceleration-structure builders (the reference builds its GAS on the device,
+ * optix_backend.h:336-358).  Both give the compressed 8-wide BVH; closest
+ * hits do not depend on the tree (ties go to the smaller triangle id). */
+typedef enum spt_build {
+    SPT_BUILD_AUTO = 0,         /* env SPT_BUILD=host|gpu, else GPU from 2M triangles up */
+    SPT_BUILD_HOST_SAH = 1,     /* binned-SAH BVH2 on the host threads, collapsed on the host */
+    SPT_BUILD_GPU_PLOC = 2      /* PLOC BVH2 + collapse on the GPU (gpu_build.hip) */
+} spt_build;
+
+/* spt_scene_create with an explicit builder (spt_build). */
+spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                               const int32_t* nrm_tri, const float* nrm, uint64_t nnrm,
+                               const int32_t* tc_tri, const float* tc, uint64_t ntc,
+                               const int32_t* mat_id, uint32_t build, spt_scene* out);
 
 /* Per-material albedo (RGB, nmat x 3).  Default: 1 for every material, as in
  * the reference (main.cpp:234,244 — Kd is read and discarded). */

@@ -15,6 +15,7 @@
 
 #include "../../include/spt.h"
 #include "bvh_build.h"
+#include "gpu_build.h"
 #include "spt_internal.h"
 
 using namespace spt;
@@ -259,6 +260,79 @@ spt_status get_event(Workspace& ws, size_t idx, hipEvent_t* out) {
     return SPT_OK;
 }
 
+// Triangle count from which SPT_BUILD_AUTO builds on the GPU.
+constexpr uint64_t kGpuBuildAutoTris = 2000000;
+
+// spt_scene_create on the GPU: upload the indexed mesh as is, assemble the
+// triangle soup, PLOC + collapse (gpu_build.hip), slot-ordered arrays.
+spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                            const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
+                            const float* tc, uint64_t ntc, const int32_t* mat_id, double t0, spt_scene* out) {
+    struct Raw {
+        int32_t *pt = nullptr, *nt = nullptr, *tt = nullptr, *mat = nullptr;
+        float *p = nullptr, *n = nullptr, *t = nullptr, *tv = nullptr;
+        ~Raw() { hfree(pt); hfree(nt); hfree(tt); hfree(mat); hfree(p); hfree(n); hfree(t); hfree(tv); }
+    } raw;
+    spt_status us = SPT_OK;
+    if (!us) us = upload(&raw.pt, pos_tri, ntri * 3 * sizeof(int32_t));
+    if (!us) us = upload(&raw.p, pos, nvert * 3 * sizeof(float));
+    if (!us && nrm_tri) us = upload(&raw.nt, nrm_tri, ntri * 3 * sizeof(int32_t));
+    if (!us && nrm_tri) us = upload(&raw.n, nrm, nnrm * 3 * sizeof(float));
+    const bool with_tc = tc_tri && tc;
+    if (!us && with_tc) us = upload(&raw.tt, tc_tri, ntri * 3 * sizeof(int32_t));
+    if (!us && with_tc) us = upload(&raw.t, tc, ntc * 2 * sizeof(float));
+    if (!us && mat_id) us = upload(&raw.mat, mat_id, ntri * sizeof(int32_t));
+    if (us) return us;
+    HIP_TRY(hipMalloc((void**)&raw.tv, sizeof(float) * 9 * std::max<uint64_t>(ntri, 1)));
+    DeviceMeshIn m{raw.pt, raw.p, raw.nt, raw.n, raw.tt, raw.t, raw.mat, (uint32_t)ntri};
+    hipStream_t s = nullptr;  // the null stream: scene creation is synchronous
+    HIP_TRY(gpu_mesh_soup(m, raw.tv, s));
+    GpuBvh8 g;
+    HIP_TRY(gpu_build_bvh8(raw.tv, (uint32_t)ntri, s, &g));
+    spt_scene_t* sc = new spt_scene_t();
+    (void)hipGetDevice(&sc->device);
+    sc->ntri = ntri;
+    sc->stack_depth = g.depth + 1;
+    sc->nodes8 = (uint4*)g.nodes8;
+    auto bail = [&](hipError_t e) {
+        (void)hipFree(g.slot2tri);
+        sc->release();
+        delete sc;
+        return fail(e == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP, "spt_scene_create (GPU build): %s",
+                    hipGetErrorString(e));
+    };
+    hipError_t e = hipSuccess;
+    if (!e) e = hipMalloc((void**)&sc->tris, sizeof(float4) * 3 * std::max<uint64_t>(ntri, 1));
+    if (!e) e = hipMalloc((void**)&sc->snrm, sizeof(float4) * 3 * std::max<uint64_t>(ntri, 1));
+    if (!e && with_tc) e = hipMalloc((void**)&sc->tc, sizeof(float) * 6 * ntri);
+    if (!e) e = hipMalloc((void**)&sc->orig2slot, sizeof(int32_t) * std::max<uint64_t>(ntri, 1));
+    if (!e) e = gpu_scene_slots(m, raw.tv, g.slot2tri, sc->tris, sc->snrm, with_tc ? sc->tc : nullptr,
+                                sc->orig2slot, s);
+    if (!e) e = hipStreamSynchronize(s);
+    if (e) return bail(e);
+    (void)hipFree(g.slot2tri);
+    const float one[3] = {1.0f, 1.0f, 1.0f};
+    if ((us = upload(&sc->albedo, one, sizeof(one)))) {
+        sc->release();
+        delete sc;
+        return us;
+    }
+    sc->nmat = 1;
+    spt_scene_stats& ss = sc->stats;
+    ss.ntri = ntri;
+    ss.nodes = g.nnodes;
+    ss.leaves = g.leaves;
+    ss.max_depth = g.depth;
+    ss.max_leaf = 3;
+    ss.bvh_width = 8;
+    ss.builder = SPT_BUILD_GPU_PLOC;
+    ss.device_bytes = (uint64_t)g.nnodes * kNode8Quads * 16 + ntri * 3 * 16 * 2 + (with_tc ? ntri * 24 : 0) + ntri * 4;
+    ss.build_ms = now_ms() - t0;
+    ss.sah_cost = g.sah_cost;
+    *out = sc;
+    return SPT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -309,22 +383,42 @@ uint32_t spt_tile_rows(uint32_t height, uint32_t tile_index, uint32_t tile_count
 spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
                             const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
                             const float* tc, uint64_t ntc, const int32_t* mat_id, spt_scene* out) {
+    return spt_scene_create_ex(pos_tri, pos, nvert, ntri, nrm_tri, nrm, nnrm, tc_tri, tc, ntc, mat_id, SPT_BUILD_AUTO,
+                               out);
+}
+
+spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                               const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
+                               const float* tc, uint64_t ntc, const int32_t* mat_id, uint32_t build,
+                               spt_scene* out) {
     if (!out) return fail(SPT_ERR_INVALID, "spt_scene_create: out is NULL");
     *out = nullptr;
     if (ntri > 0 && (!pos_tri || !pos)) return fail(SPT_ERR_INVALID, "spt_scene_create: NULL positions");
     if (ntri >= kMaxTriangles) return fail(SPT_ERR_LIMIT, "spt_scene_create: %llu triangles exceeds 2^28", (unsigned long long)ntri);
     if (nrm_tri && !nrm && nnrm) return fail(SPT_ERR_INVALID, "spt_scene_create: normal indices without normals");
+    if (build > SPT_BUILD_GPU_PLOC) return fail(SPT_ERR_INVALID, "spt_scene_create: unknown builder %u", build);
     spt_status st = ensure_device();
     if (st) return st;
+    if (build == SPT_BUILD_AUTO) {
+        const char* b = std::getenv("SPT_BUILD");
+        if (b && std::strcmp(b, "gpu") == 0) build = SPT_BUILD_GPU_PLOC;
+        else if (b && std::strcmp(b, "host") == 0) build = SPT_BUILD_HOST_SAH;
+        else build = ntri >= kGpuBuildAutoTris ? SPT_BUILD_GPU_PLOC : SPT_BUILD_HOST_SAH;
+    }
+    const char* kind = std::getenv("SPT_BVH");
+    const bool use8 = !(kind && std::strcmp(kind, "2") == 0);
+    if (build == SPT_BUILD_GPU_PLOC && !use8) build = SPT_BUILD_HOST_SAH;  // the GPU builder makes BVH8 only
     const double t0 = now_ms();
-    std::vector<float> tv((size_t)ntri * 9);
+    const bool host = build == SPT_BUILD_HOST_SAH;
+    std::vector<float> tv(host ? (size_t)ntri * 9 : 0);
     for (uint64_t t = 0; t < ntri; t++) {
         for (int k = 0; k < 3; k++) {
             int64_t pi = pos_tri[t * 3 + k];
             if (pi < 0 || (uint64_t)pi >= nvert)
                 return fail(SPT_ERR_INVALID, "spt_scene_create: triangle %llu position index %lld out of range [0,%llu)",
                             (unsigned long long)t, (long long)pi, (unsigned long long)nvert);
-            for (int c = 0; c < 3; c++) tv[t * 9 + k * 3 + c] = pos[pi * 3 + c];
+            if (host)
+                for (int c = 0; c < 3; c++) tv[t * 9 + k * 3 + c] = pos[pi * 3 + c];
         }
         if (nrm_tri)
             for (int k = 0; k < 3; k++) {
@@ -341,10 +435,10 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
                                 (unsigned long long)t, (long long)ti);
             }
     }
+    if (!host)
+        return create_scene_gpu(pos_tri, pos, nvert, ntri, nrm_tri, nrm, nnrm, tc_tri, tc, ntc, mat_id, t0, out);
     // Acceleration structure: the compressed 8-wide BVH by default; SPT_BVH=2
     // selects the plain BVH2 (kept as the simple reference layout).
-    const char* kind = std::getenv("SPT_BVH");
-    const bool use8 = !(kind && std::strcmp(kind, "2") == 0);
     BvhBuildResult bvh;
     Bvh8BuildResult bvh8;
     if (use8)
@@ -424,6 +518,7 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
                       h_tc.size() * 4 + h_o2s.size() * 4;
     ss.build_ms = t1 - t0;
     ss.sah_cost = use8 ? bvh8.sah_cost : bvh.sah_cost;
+    ss.builder = SPT_BUILD_HOST_SAH;
     *out = sc;
     return SPT_OK;
 }

@@ -1,0 +1,50 @@
+// gpu_build.h — acceleration structure built on the GPU (gpu_build.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spt {
+
+struct GpuBvh8 {
+    uint32_t* nodes8 = nullptr;    // device, kNode8Quads * 4 words per node (bvh_build.h layout)
+    uint32_t* slot2tri = nullptr;  // device, triangle slot -> original triangle id
+    uint32_t nnodes = 0;
+    uint32_t depth = 0;            // deepest node level (root = 1)
+    uint64_t leaves = 0;
+    uint32_t ploc_iterations = 0;
+    double sah_cost = 0.0;         // of the BVH2 (bvh_build.cpp accounting)
+    double bvh2_ms = 0.0;          // PLOC part
+    double build_ms = 0.0;         // whole build (host wall time, synchronised)
+};
+
+// d_tv: device, ntri x 9 floats (v0 v1 v2).  On success the caller owns
+// out->nodes8 and out->slot2tri (hipFree).  Synchronises stream s.
+hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out);
+
+}  // namespace spt
+
+namespace spt {
+
+// Raw indexed mesh on the device (spt_scene_create's arrays, uploaded as is).
+struct DeviceMeshIn {
+    const int32_t* pos_tri;  // 3 per triangle
+    const float* pos;        // 3 per vertex
+    const int32_t* nrm_tri;  // 3 per triangle or null (-1 = missing: geometric normal)
+    const float* nrm;
+    const int32_t* tc_tri;   // 3 per triangle or null
+    const float* tc;
+    const int32_t* mat_id;   // per triangle or null (material 0)
+    uint32_t ntri;
+};
+
+// Triangle soup (ntri x 9 floats) from the indexed mesh.
+hipError_t gpu_mesh_soup(const DeviceMeshIn& m, float* tv, hipStream_t s);
+
+// Slot-ordered scene arrays from the build's slot2tri (the device side of
+// spt_scene_create's host loop): tris 3 x float4 per slot (v + original id
+// bits), snrm 3 x float4 (normals + material id bits), tc 6 floats per slot
+// (may be null), orig2slot.
+hipError_t gpu_scene_slots(const DeviceMeshIn& m, const float* tv, const uint32_t* slot2tri, float4* tris,
+                           float4* snrm, float* tc, int32_t* orig2slot, hipStream_t s);
+
+}  // namespace spt

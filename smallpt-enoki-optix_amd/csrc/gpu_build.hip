@@ -1,0 +1,656 @@
+// gpu_build.hip — the acceleration structure built on the GPU (gfx950):
+// PLOC BVH2 (Meister & Bittner, "Parallel Locally-Ordered Clustering for
+// Bounding Volume Hierarchy Construction", TVCG 2018) over 63-bit Morton
+// order, then a level-by-level collapse into the compressed 8-wide layout of
+// bvh_build.h (the same greedy collapse, octant slot order and conservative
+// 8-bit quantisation as bvh8_build.cpp, one thread per BVH8 node).
+//
+// Replaces the reference's on-device GAS build (optixAccelBuild +
+// optixAccelCompact, optix_backend.h:336-358); the host binned-SAH build
+// (bvh_build.cpp) stays as the default for small scenes.  Every step is
+// deterministic: node and triangle offsets come from prefix sums, never from
+// atomics, so a scene always gets the same tree.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
+#include "gpu_build.h"
+#include "spt_internal.h"
+
+namespace spt {
+namespace {
+
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kLeafMaxTris = 3;  // a BVH8 leaf holds up to 3 triangles
+constexpr int kDefaultRadius = 16;
+
+inline uint32_t blocks(uint64_t n, uint32_t b = kBlock) { return (uint32_t)((n + b - 1) / b); }
+
+// order-preserving float <-> uint map, for atomicMin/Max on floats
+__device__ __forceinline__ uint32_t f2ord(float f) {
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(uint32_t u) {
+    return __builtin_bit_cast(float, (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+__device__ __forceinline__ float half_area(float4 lo, float4 hi) {
+    const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__device__ __forceinline__ uint64_t spread21(uint64_t x) {
+    x &= 0x1fffff;
+    x = (x | x << 32) & 0x1f00000000ffffull;
+    x = (x | x << 16) & 0x1f0000ff0000ffull;
+    x = (x | x << 8) & 0x100f00f00f00f00full;
+    x = (x | x << 4) & 0x10c30c30c30c30c3ull;
+    x = (x | x << 2) & 0x1249249249249249ull;
+    return x;
+}
+
+// Per-triangle box, and the centroid bounds (ordered-uint atomics, 6 words).
+__global__ __launch_bounds__(kBlock) void tri_box_kernel(const float* __restrict__ tv, uint32_t n,
+                                                         float4* __restrict__ lo, float4* __restrict__ hi,
+                                                         uint32_t* __restrict__ cb) {
+    __shared__ uint32_t s[6];
+    if (threadIdx.x < 6) s[threadIdx.x] = threadIdx.x < 3 ? 0xffffffffu : 0u;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) {
+        const float* v = tv + (size_t)i * 9;
+        float l[3], h[3];
+        for (int a = 0; a < 3; a++) {
+            l[a] = fminf(fminf(v[a], v[3 + a]), v[6 + a]);
+            h[a] = fmaxf(fmaxf(v[a], v[3 + a]), v[6 + a]);
+        }
+        lo[i] = make_float4(l[0], l[1], l[2], 0.0f);
+        hi[i] = make_float4(h[0], h[1], h[2], 0.0f);
+        for (int a = 0; a < 3; a++) {
+            const float c = 0.5f * (l[a] + h[a]);
+            atomicMin(&s[a], f2ord(c));
+            atomicMax(&s[3 + a], f2ord(c));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) atomicMin(&cb[threadIdx.x], s[threadIdx.x]);
+    else if (threadIdx.x < 6) atomicMax(&cb[threadIdx.x], s[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kBlock) void morton_kernel(const float4* __restrict__ lo, const float4* __restrict__ hi,
+                                                        uint32_t n, const uint32_t* __restrict__ cb,
+                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 l = lo[i], h = hi[i];
+    const float c[3] = {0.5f * (l.x + h.x), 0.5f * (l.y + h.y), 0.5f * (l.z + h.z)};
+    uint64_t key = 0;
+    for (int a = 0; a < 3; a++) {
+        const float b0 = ord2f(cb[a]), b1 = ord2f(cb[3 + a]);
+        const float ext = b1 - b0;
+        float t = ext > 0.0f ? (c[a] - b0) / ext : 0.5f;
+        t = fminf(fmaxf(t, 0.0f), 1.0f);
+        key |= spread21((uint64_t)(t * 2097151.0f)) << (2 - a);
+    }
+    keys[i] = key;
+    vals[i] = i;
+}
+
+// Clusters start as the Morton-sorted triangles (BVH2 leaf node id = triangle id).
+__global__ __launch_bounds__(kBlock) void init_clusters_kernel(const uint32_t* __restrict__ order, uint32_t n,
+                                                               const float4* __restrict__ lo,
+                                                               const float4* __restrict__ hi,
+                                                               uint32_t* __restrict__ cnode, float4* __restrict__ clo,
+                                                               float4* __restrict__ chi) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = order[i];
+    cnode[i] = t;
+    clo[i] = lo[t];
+    chi[i] = hi[t];
+}
+
+__global__ __launch_bounds__(kBlock) void leaf_ones_kernel(uint32_t* __restrict__ ntris, uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) ntris[i] = 1u;
+}
+
+// Nearest neighbour within +-r in the cluster array: the one whose merged box
+// has the smallest area; ties go to the smaller index, so the candidate pair
+// with the smallest (area, lower index, higher index) is always mutual and
+// every iteration merges at least one pair.
+template <int kPlocRadius>  // neighbours searched on each side (PLOC's r)
+__global__ __launch_bounds__(kBlock) void nn_kernel(const float4* __restrict__ clo, const float4* __restrict__ chi,
+                                                    uint32_t n, uint32_t* __restrict__ nn) {
+    __shared__ float4 slo[kBlock + 2 * kPlocRadius], shi[kBlock + 2 * kPlocRadius];
+    const int64_t b0 = (int64_t)blockIdx.x * kBlock - kPlocRadius;
+    for (uint32_t k = threadIdx.x; k < kBlock + 2 * kPlocRadius; k += kBlock) {
+        const int64_t j = b0 + k;
+        if (j >= 0 && j < (int64_t)n) {
+            slo[k] = clo[j];
+            shi[k] = chi[j];
+        }
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t li = threadIdx.x + kPlocRadius;
+    const float4 l = slo[li], h = shi[li];
+    float best = INFINITY;
+    uint32_t bj = i;
+    const int64_t jlo = std::max<int64_t>(0, (int64_t)i - kPlocRadius);
+    const int64_t jhi = std::min<int64_t>((int64_t)n - 1, (int64_t)i + kPlocRadius);
+    for (int64_t j = jlo; j <= jhi; j++) {
+        if (j == (int64_t)i) continue;
+        const uint32_t lj = (uint32_t)(j - b0);
+        const float4 ol = slo[lj], oh = shi[lj];
+        const float a = half_area(make_float4(fminf(l.x, ol.x), fminf(l.y, ol.y), fminf(l.z, ol.z), 0.0f),
+                                  make_float4(fmaxf(h.x, oh.x), fmaxf(h.y, oh.y), fmaxf(h.z, oh.z), 0.0f));
+        if (a < best) {
+            best = a;
+            bj = (uint32_t)j;
+        }
+    }
+    nn[i] = bj;
+}
+
+// flags[i] = merge << 32 | keep: cluster i opens a merge with its mutual
+// nearest neighbour (the lower of the pair), or survives (all but the higher).
+__global__ __launch_bounds__(kBlock) void merge_flags_kernel(const uint32_t* __restrict__ nn, uint32_t n,
+                                                             uint64_t* __restrict__ flags) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = nn[i];
+    const bool mutual = j != i && nn[j] == i;
+    const uint64_t merge = mutual && i < j, keep = !(mutual && i > j);
+    flags[i] = (merge << 32) | keep;
+}
+
+// Merge and compact in one pass.  New inner node ids: leaves occupy [0, ntri),
+// inner nodes are numbered in creation order from ntri.
+__global__ __launch_bounds__(kBlock) void merge_compact_kernel(
+    const uint32_t* __restrict__ nn, const uint64_t* __restrict__ flags, const uint64_t* __restrict__ scan,
+    uint32_t n, uint32_t node_base, const uint32_t* __restrict__ cnode, const float4* __restrict__ clo,
+    const float4* __restrict__ chi, uint32_t* __restrict__ onode, float4* __restrict__ olo,
+    float4* __restrict__ ohi, float4* __restrict__ nlo, float4* __restrict__ nhi, int2* __restrict__ nkids,
+    uint32_t* __restrict__ ntris) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t f = flags[i];
+    if (!(f & 1u)) return;
+    const uint32_t dst = (uint32_t)(scan[i] & 0xffffffffu);
+    if (f >> 32) {
+        const uint32_t j = nn[i];
+        const uint32_t id = node_base + (uint32_t)(scan[i] >> 32);
+        const float4 a = clo[i], b = clo[j], c = chi[i], d = chi[j];
+        const float4 l = make_float4(fminf(a.x, b.x), fminf(a.y, b.y), fminf(a.z, b.z), 0.0f);
+        const float4 h = make_float4(fmaxf(c.x, d.x), fmaxf(c.y, d.y), fmaxf(c.z, d.z), 0.0f);
+        const uint32_t ci = cnode[i], cj = cnode[j];
+        nlo[id] = l;
+        nhi[id] = h;
+        nkids[id] = make_int2((int)ci, (int)cj);
+        ntris[id] = ntris[ci] + ntris[cj];
+        onode[dst] = id;
+        olo[dst] = l;
+        ohi[dst] = h;
+    } else {
+        onode[dst] = cnode[i];
+        olo[dst] = clo[i];
+        ohi[dst] = chi[i];
+    }
+}
+
+// totals of an exclusive scan: out = scan[n-1] + flags[n-1]
+__global__ void scan_total_kernel(const uint64_t* __restrict__ flags, const uint64_t* __restrict__ scan, uint32_t n,
+                                  uint64_t* __restrict__ out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *out = n ? scan[n - 1] + flags[n - 1] : 0ull;
+}
+
+// SAH cost of the BVH2 (bvh_build.cpp's accounting: inner nodes 1, triangles
+// 1, both weighted by area / root area).
+__global__ __launch_bounds__(kBlock) void sah_kernel(const float4* __restrict__ lo, const float4* __restrict__ hi,
+                                                     uint32_t nnodes, uint32_t ntri, uint32_t root,
+                                                     double* __restrict__ out) {
+    __shared__ double s[kBlock];
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const double ra = (double)half_area(lo[root], hi[root]);
+    s[threadIdx.x] = (i < nnodes && ra > 0.0) ? (double)half_area(lo[i], hi[i]) / ra : 0.0;
+    __syncthreads();
+    for (uint32_t k = kBlock / 2; k > 0; k >>= 1) {
+        if (threadIdx.x < k) s[threadIdx.x] += s[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(out, s[0]);
+    (void)ntri;
+}
+
+// ---------------------------------------------------------------- collapse
+struct CollapseArgs {
+    const float4* lo;
+    const float4* hi;
+    const int2* kids2;       // BVH2 inner children (node id >= ntri)
+    const uint32_t* ntris;   // triangles under each BVH2 node
+    uint32_t ntri;
+    const uint32_t* queue;   // BVH2 node of each BVH8 node of this level (root-leaf: a leaf id)
+    uint32_t count;
+    uint32_t* kids8;         // [count][8] chosen BVH2 children, 0xffffffff = empty
+    uint64_t* counts;        // inner << 32 | leaf triangles
+};
+
+__device__ __forceinline__ bool leafable(const CollapseArgs& a, uint32_t node) {
+    return node < a.ntri || a.ntris[node] <= kLeafMaxTris;
+}
+
+// Pass A: one thread per BVH8 node of the level; greedy collapse (open the
+// largest-area child that cannot be a leaf while fewer than 8 children).
+__global__ __launch_bounds__(kBlock) void collapse_pick_kernel(CollapseArgs a) {
+    const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= a.count) return;
+    const uint32_t root = a.queue[e];
+    uint32_t k[8];
+    uint32_t nk = 0;
+    if (root < a.ntri) {  // single-triangle scene: the root is a leaf
+        k[nk++] = root;
+    } else {
+        const int2 c = a.kids2[root];
+        k[nk++] = (uint32_t)c.x;
+        k[nk++] = (uint32_t)c.y;
+    }
+    while (nk < 8) {
+        int best = -1;
+        float ba = -1.0f;
+        for (uint32_t i = 0; i < nk; i++)
+            if (!leafable(a, k[i])) {
+                const float ar = half_area(a.lo[k[i]], a.hi[k[i]]);
+                if (ar > ba) { ba = ar; best = (int)i; }
+            }
+        if (best < 0) break;
+        const int2 c = a.kids2[k[best]];
+        k[best] = (uint32_t)c.x;
+        k[nk++] = (uint32_t)c.y;
+    }
+    uint32_t ninner = 0, nleaf = 0;
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t v = i < nk ? k[i] : 0xffffffffu;
+        a.kids8[(size_t)e * 8 + i] = v;
+        if (i < nk) {
+            if (leafable(a, v)) nleaf += a.ntris[v];
+            else ninner++;
+        }
+    }
+    a.counts[e] = ((uint64_t)ninner << 32) | nleaf;
+}
+
+struct EmitArgs {
+    CollapseArgs c;
+    const uint64_t* scan;     // exclusive scan of counts
+    uint32_t next_first;      // BVH8 index of the next level's first node
+    uint32_t tri_first;       // first triangle slot of this level
+    uint32_t level_first;     // BVH8 index of this level's first node
+    uint32_t* nodes8;         // kNode8Quads * 4 words per node
+    uint32_t* slot2tri;
+    uint32_t* next_queue;
+    unsigned long long* leaves;  // leaf slots (statistics)
+};
+
+// Pass B: octant slot order, quantisation frame, node words, leaf triangles
+// and the next level's queue (same arithmetic as bvh8_build.cpp emit()).
+__global__ __launch_bounds__(kBlock) void collapse_emit_kernel(EmitArgs a) {
+    const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
+    if (e >= a.c.count) return;
+    uint32_t k[8];
+    uint32_t nk = 0;
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t v = a.c.kids8[(size_t)e * 8 + i];
+        if (v != 0xffffffffu) k[nk++] = v;
+    }
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < nk; i++) {
+        const float4 l = a.c.lo[k[i]], h = a.c.hi[k[i]];
+        lo[0] = fminf(lo[0], l.x); lo[1] = fminf(lo[1], l.y); lo[2] = fminf(lo[2], l.z);
+        hi[0] = fmaxf(hi[0], h.x); hi[1] = fmaxf(hi[1], h.y); hi[2] = fmaxf(hi[2], h.z);
+    }
+    double ctr[3];
+    for (int ax = 0; ax < 3; ax++) ctr[ax] = 0.5 * ((double)lo[ax] + (double)hi[ax]);
+    // greedy octant assignment: repeatedly the cheapest free (kid, slot) pair
+    int kid_in[8];
+    for (int s = 0; s < 8; s++) kid_in[s] = -1;
+    uint32_t kdone = 0;
+    for (uint32_t m = 0; m < nk; m++) {
+        double bc = INFINITY;
+        int bk = -1, bs = -1;
+        for (uint32_t i = 0; i < nk; i++) {
+            if ((kdone >> i) & 1u) continue;
+            const float4 l = a.c.lo[k[i]], h = a.c.hi[k[i]];
+            const double d0 = 0.5 * ((double)l.x + (double)h.x) - ctr[0];
+            const double d1 = 0.5 * ((double)l.y + (double)h.y) - ctr[1];
+            const double d2 = 0.5 * ((double)l.z + (double)h.z) - ctr[2];
+            for (int s = 0; s < 8; s++) {
+                if (kid_in[s] >= 0) continue;
+                const double c = ((s & 1) ? -d0 : d0) + ((s & 2) ? -d1 : d1) + ((s & 4) ? -d2 : d2);
+                if (c < bc) { bc = c; bk = (int)i; bs = s; }
+            }
+        }
+        if (bk < 0) {  // NaN costs: first free kid into the first free slot
+            for (uint32_t i = 0; i < nk; i++)
+                if (!((kdone >> i) & 1u)) { bk = (int)i; break; }
+            for (int s = 0; s < 8; s++)
+                if (kid_in[s] < 0) { bs = s; break; }
+        }
+        kdone |= 1u << bk;
+        kid_in[bs] = bk;
+    }
+    const uint32_t idx = a.level_first + e;
+    uint32_t* w = a.nodes8 + (size_t)idx * kNode8Quads * 4;
+    int ebias[3];
+    for (int ax = 0; ax < 3; ax++) {
+        const double ext = (double)hi[ax] - (double)lo[ax];
+        int ex = -100;
+        if (ext > 0.0) {
+            ex = (int)ceil(log2(ext / 255.0));
+            while (ldexp(255.0, ex) < ext) ex++;
+            ex = max(ex, -100);
+        }
+        ebias[ax] = ex + 127;
+        w[ax] = __builtin_bit_cast(uint32_t, lo[ax]);
+    }
+    const uint64_t sc = a.scan[e];
+    const uint32_t child_base = a.next_first + (uint32_t)(sc >> 32);
+    const uint32_t tri_base = a.tri_first + (uint32_t)(sc & 0xffffffffu);
+    uint32_t imask = 0, toff = 0, r = 0, nleaves = 0;
+    uint8_t meta[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint8_t q[6][8];
+    for (int s = 0; s < 8; s++)
+        for (int ax = 0; ax < 3; ax++) { q[ax][s] = 255; q[3 + ax][s] = 0; }  // empty: inverted
+    for (int s = 0; s < 8; s++) {
+        const int kk = kid_in[s];
+        if (kk < 0) continue;
+        const uint32_t node = k[kk];
+        const float4 l = a.c.lo[node], h = a.c.hi[node];
+        const float kl[3] = {l.x, l.y, l.z}, kh[3] = {h.x, h.y, h.z};
+        for (int ax = 0; ax < 3; ax++) {
+            const double step = ldexp(1.0, ebias[ax] - 127);
+            double ql = floor(((double)kl[ax] - (double)lo[ax]) / step);
+            double qh = ceil(((double)kh[ax] - (double)lo[ax]) / step);
+            if (!(ql >= 0.0)) ql = 0.0;
+            if (!(qh <= 255.0)) qh = 255.0;
+            if (ql > 255.0) ql = 255.0;
+            if (qh < 0.0) qh = 0.0;
+            q[ax][s] = (uint8_t)ql;
+            q[3 + ax][s] = (uint8_t)qh;
+        }
+        if (!leafable(a.c, node)) {
+            imask |= 1u << s;
+            meta[s] = (uint8_t)(0x20u | (24u + (uint32_t)s));
+            a.next_queue[child_base - a.next_first + r] = node;
+            r++;
+        } else {
+            // the <= 3 triangles of the subtree, left to right
+            uint32_t stack[4], sp = 0, cnt = 0;
+            stack[sp++] = node;
+            while (sp) {
+                const uint32_t x = stack[--sp];
+                if (x < a.c.ntri) {
+                    a.slot2tri[tri_base + toff + cnt] = x;
+                    cnt++;
+                } else {
+                    const int2 c = a.c.kids2[x];
+                    stack[sp++] = (uint32_t)c.y;
+                    stack[sp++] = (uint32_t)c.x;
+                }
+            }
+            meta[s] = (uint8_t)((((1u << cnt) - 1u) << 5) | toff);
+            toff += cnt;
+            nleaves++;
+        }
+    }
+    w[3] = (uint32_t)ebias[0] | ((uint32_t)ebias[1] << 8) | ((uint32_t)ebias[2] << 16) | (imask << 24);
+    w[4] = imask ? child_base : 0u;
+    w[5] = tri_base;
+    w[6] = (uint32_t)meta[0] | ((uint32_t)meta[1] << 8) | ((uint32_t)meta[2] << 16) | ((uint32_t)meta[3] << 24);
+    w[7] = (uint32_t)meta[4] | ((uint32_t)meta[5] << 8) | ((uint32_t)meta[6] << 16) | ((uint32_t)meta[7] << 24);
+    for (int p = 0; p < 6; p++) {
+        w[8 + 2 * p] = (uint32_t)q[p][0] | ((uint32_t)q[p][1] << 8) | ((uint32_t)q[p][2] << 16) |
+                       ((uint32_t)q[p][3] << 24);
+        w[9 + 2 * p] = (uint32_t)q[p][4] | ((uint32_t)q[p][5] << 8) | ((uint32_t)q[p][6] << 16) |
+                       ((uint32_t)q[p][7] << 24);
+    }
+    for (uint32_t z = 20; z < kNode8Quads * 4; z++) w[z] = 0u;
+    atomicAdd(a.leaves, (unsigned long long)nleaves);
+}
+
+template <typename T>
+hipError_t dmalloc(T** p, size_t count) {
+    return hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1));
+}
+
+struct Temp {
+    std::vector<void*> ptrs;
+    ~Temp() {
+        for (void* p : ptrs) (void)hipFree(p);
+    }
+    template <typename T>
+    hipError_t get(T** p, size_t count) {
+        hipError_t e = dmalloc(p, count);
+        if (e == hipSuccess) ptrs.push_back((void*)*p);
+        return e;
+    }
+};
+
+#define GB_TRY(call)                          \
+    do {                                      \
+        hipError_t e_ = (call);               \
+        if (e_ != hipSuccess) return e_;      \
+    } while (0)
+
+}  // namespace
+
+hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out) {
+    *out = GpuBvh8();
+    if (ntri == 0) return hipSuccess;
+    const auto t0 = std::chrono::steady_clock::now();
+    Temp tmp;
+    const uint32_t nnodes = 2 * ntri - 1;
+    float4 *lo, *hi, *clo[2], *chi[2];
+    int2* kids2;
+    uint32_t *ntris, *cnode[2], *nn, *cb, *vals[2];
+    uint64_t *keys[2], *flags, *scan, *total;
+    unsigned long long* leaves;
+    double* sah;
+    GB_TRY(tmp.get(&lo, nnodes));
+    GB_TRY(tmp.get(&hi, nnodes));
+    GB_TRY(tmp.get(&kids2, nnodes));
+    GB_TRY(tmp.get(&ntris, nnodes));
+    for (int b = 0; b < 2; b++) {
+        GB_TRY(tmp.get(&clo[b], ntri));
+        GB_TRY(tmp.get(&chi[b], ntri));
+        GB_TRY(tmp.get(&cnode[b], ntri));
+        GB_TRY(tmp.get(&keys[b], ntri));
+        GB_TRY(tmp.get(&vals[b], ntri));
+    }
+    GB_TRY(tmp.get(&nn, ntri));
+    GB_TRY(tmp.get(&flags, ntri));
+    GB_TRY(tmp.get(&scan, ntri));
+    GB_TRY(tmp.get(&total, 2));
+    GB_TRY(tmp.get(&cb, 6));
+    GB_TRY(tmp.get(&sah, 1));
+    GB_TRY(tmp.get(&leaves, 1));
+    GB_TRY(hipMemsetAsync(leaves, 0, sizeof(unsigned long long), s));
+
+    // leaves, Morton order
+    const uint32_t cb_init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+    GB_TRY(hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(tri_box_kernel, dim3(blocks(ntri)), dim3(kBlock), 0, s, d_tv, ntri, lo, hi, cb);
+    hipLaunchKernelGGL(morton_kernel, dim3(blocks(ntri)), dim3(kBlock), 0, s, lo, hi, ntri, cb, keys[0], vals[0]);
+    GB_TRY(hipGetLastError());
+    {
+        hipcub::DoubleBuffer<uint64_t> dk(keys[0], keys[1]);
+        hipcub::DoubleBuffer<uint32_t> dv(vals[0], vals[1]);
+        size_t bytes = 0;
+        GB_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, dk, dv, (int)ntri, 0, 63, s));
+        void* ws = nullptr;
+        GB_TRY(tmp.get((char**)&ws, bytes));
+        GB_TRY(hipcub::DeviceRadixSort::SortPairs(ws, bytes, dk, dv, (int)ntri, 0, 63, s));
+        hipLaunchKernelGGL(init_clusters_kernel, dim3(blocks(ntri)), dim3(kBlock), 0, s, dv.Current(), ntri, lo, hi,
+                           cnode[0], clo[0], chi[0]);
+    }
+    hipLaunchKernelGGL(leaf_ones_kernel, dim3(blocks(ntri)), dim3(kBlock), 0, s, ntris, ntri);  // 1 tri per leaf
+    GB_TRY(hipGetLastError());
+
+    // PLOC iterations (search radius: env SPT_PLOC_RADIUS = 8, 16, 32 or 64)
+    const char* rv = std::getenv("SPT_PLOC_RADIUS");
+    const int radius = rv ? std::atoi(rv) : kDefaultRadius;
+    size_t scan_bytes = 0;
+    GB_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, flags, scan, (int)ntri, s));
+    void* scan_ws = nullptr;
+    GB_TRY(tmp.get((char**)&scan_ws, scan_bytes));
+    uint32_t n = ntri, cur = 0, node_base = ntri, iters = 0;
+    uint64_t tot = 0;
+    while (n > 1) {
+        switch (radius) {
+            case 8: hipLaunchKernelGGL(nn_kernel<8>, dim3(blocks(n)), dim3(kBlock), 0, s, clo[cur], chi[cur], n, nn); break;
+            case 32: hipLaunchKernelGGL(nn_kernel<32>, dim3(blocks(n)), dim3(kBlock), 0, s, clo[cur], chi[cur], n, nn); break;
+            case 64: hipLaunchKernelGGL(nn_kernel<64>, dim3(blocks(n)), dim3(kBlock), 0, s, clo[cur], chi[cur], n, nn); break;
+            default: hipLaunchKernelGGL(nn_kernel<16>, dim3(blocks(n)), dim3(kBlock), 0, s, clo[cur], chi[cur], n, nn);
+        }
+        hipLaunchKernelGGL(merge_flags_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, nn, n, flags);
+        GB_TRY(hipGetLastError());
+        GB_TRY(hipcub::DeviceScan::ExclusiveSum(scan_ws, scan_bytes, flags, scan, (int)n, s));
+        hipLaunchKernelGGL(merge_compact_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, nn, flags, scan, n, node_base,
+                           cnode[cur], clo[cur], chi[cur], cnode[1 - cur], clo[1 - cur], chi[1 - cur], lo, hi, kids2,
+                           ntris);
+        hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, s, flags, scan, n, total);
+        GB_TRY(hipGetLastError());
+        GB_TRY(hipMemcpyAsync(&tot, total, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        GB_TRY(hipStreamSynchronize(s));
+        const uint32_t merged = (uint32_t)(tot >> 32), kept = (uint32_t)(tot & 0xffffffffu);
+        if (merged == 0) return hipErrorUnknown;  // cannot happen (see nn_kernel)
+        node_base += merged;
+        n = kept;
+        cur = 1 - cur;
+        iters++;
+    }
+    uint32_t root = 0;
+    GB_TRY(hipMemcpyAsync(&root, cnode[cur], sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GB_TRY(hipMemsetAsync(sah, 0, sizeof(double), s));
+    hipLaunchKernelGGL(sah_kernel, dim3(blocks(nnodes)), dim3(kBlock), 0, s, lo, hi, nnodes, ntri, root, sah);
+    GB_TRY(hipGetLastError());
+    GB_TRY(hipMemcpyAsync(&out->sah_cost, sah, sizeof(double), hipMemcpyDeviceToHost, s));
+    GB_TRY(hipStreamSynchronize(s));
+    out->bvh2_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    out->ploc_iterations = iters;
+
+    // Collapse, level by level.  At most ntri BVH8 nodes (every node holds
+    // at least two children or is the single root).
+    uint32_t *queue[2], *kids8, *nodes8, *slot2tri;
+    uint64_t* counts;
+    const size_t max8 = std::max<size_t>(1, ntri);
+    GB_TRY(tmp.get(&queue[0], max8));
+    GB_TRY(tmp.get(&queue[1], max8));
+    GB_TRY(tmp.get(&kids8, max8 * 8));
+    GB_TRY(tmp.get(&counts, max8));
+    GB_TRY(dmalloc(&nodes8, max8 * kNode8Quads * 4));
+    GB_TRY(dmalloc(&slot2tri, ntri));
+    GB_TRY(hipMemcpyAsync(queue[0], &root, sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    uint32_t count = 1, level_first = 0, next_first = 1, tri_first = 0, depth = 0, q = 0;
+    size_t scan8_bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan8_bytes, counts, scan, (int)max8, s);
+    void* scan8_ws = nullptr;
+    hipError_t err = tmp.get((char**)&scan8_ws, scan8_bytes);
+    while (err == hipSuccess && count > 0) {
+        CollapseArgs c{lo, hi, kids2, ntris, ntri, queue[q], count, kids8, counts};
+        hipLaunchKernelGGL(collapse_pick_kernel, dim3(blocks(count)), dim3(kBlock), 0, s, c);
+        if ((err = hipGetLastError())) break;
+        if ((err = hipcub::DeviceScan::ExclusiveSum(scan8_ws, scan8_bytes, counts, scan, (int)count, s))) break;
+        EmitArgs ea{c, scan, next_first, tri_first, level_first, nodes8, slot2tri, queue[1 - q], leaves};
+        hipLaunchKernelGGL(collapse_emit_kernel, dim3(blocks(count)), dim3(kBlock), 0, s, ea);
+        hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, s, counts, scan, count, total);
+        if ((err = hipGetLastError())) break;
+        if ((err = hipMemcpyAsync(&tot, total, sizeof(uint64_t), hipMemcpyDeviceToHost, s))) break;
+        if ((err = hipStreamSynchronize(s))) break;
+        depth++;
+        level_first = next_first;
+        count = (uint32_t)(tot >> 32);
+        next_first += count;
+        tri_first += (uint32_t)(tot & 0xffffffffu);
+        q = 1 - q;
+    }
+    if (err == hipSuccess && tri_first != ntri) err = hipErrorUnknown;  // every triangle in exactly one leaf
+    if (err != hipSuccess) {
+        (void)hipFree(nodes8);
+        (void)hipFree(slot2tri);
+        return err;
+    }
+    unsigned long long nleaves = 0;
+    (void)hipMemcpy(&nleaves, leaves, sizeof(nleaves), hipMemcpyDeviceToHost);
+    out->leaves = nleaves;
+    out->nodes8 = nodes8;
+    out->slot2tri = slot2tri;
+    out->nnodes = level_first;  // == next_first after the last (empty) level
+    out->depth = depth;
+    out->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return hipSuccess;
+}
+
+}  // namespace spt
+
+namespace spt {
+namespace {
+
+__global__ __launch_bounds__(kBlock) void mesh_soup_kernel(DeviceMeshIn m, float* __restrict__ tv) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= m.ntri) return;
+    for (int k = 0; k < 3; k++) {
+        const int64_t pi = m.pos_tri[(size_t)t * 3 + k];
+        for (int c = 0; c < 3; c++) tv[(size_t)t * 9 + k * 3 + c] = m.pos[pi * 3 + c];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void scene_slots_kernel(DeviceMeshIn m, const float* __restrict__ tv,
+                                                             const uint32_t* __restrict__ slot2tri,
+                                                             float4* __restrict__ tris, float4* __restrict__ snrm,
+                                                             float* __restrict__ tc, int32_t* __restrict__ o2s) {
+    const uint32_t sl = blockIdx.x * kBlock + threadIdx.x;
+    if (sl >= m.ntri) return;
+    const uint32_t t = slot2tri[sl];
+    o2s[t] = (int32_t)sl;
+    const float* v = tv + (size_t)t * 9;
+    for (int k = 0; k < 3; k++)
+        tris[(size_t)sl * 3 + k] = make_float4(v[k * 3], v[k * 3 + 1], v[k * 3 + 2], k == 0 ? u2f(t) : 0.0f);
+    // geometric normal fallback for a missing vertex normal (as spt_scene_create's host loop)
+    const V3 g = normalize(cross(v3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), v3(v[6] - v[0], v[7] - v[1], v[8] - v[2])));
+    const int32_t mat = m.mat_id ? m.mat_id[t] : 0;
+    for (int k = 0; k < 3; k++) {
+        const int64_t ni = m.nrm_tri ? m.nrm_tri[(size_t)t * 3 + k] : -1;
+        const V3 nv = ni >= 0 ? v3(m.nrm[ni * 3], m.nrm[ni * 3 + 1], m.nrm[ni * 3 + 2]) : g;
+        snrm[(size_t)sl * 3 + k] = make_float4(nv.x, nv.y, nv.z, k == 0 ? __builtin_bit_cast(float, mat) : 0.0f);
+    }
+    if (tc)
+        for (int k = 0; k < 3; k++) {
+            const int64_t ti = m.tc_tri[(size_t)t * 3 + k];
+            tc[(size_t)sl * 6 + k * 2] = ti >= 0 ? m.tc[ti * 2] : 0.0f;
+            tc[(size_t)sl * 6 + k * 2 + 1] = ti >= 0 ? m.tc[ti * 2 + 1] : 0.0f;
+        }
+}
+
+}  // namespace
+
+hipError_t gpu_mesh_soup(const DeviceMeshIn& m, float* tv, hipStream_t s) {
+    if (m.ntri == 0) return hipSuccess;
+    hipLaunchKernelGGL(mesh_soup_kernel, dim3(blocks(m.ntri)), dim3(kBlock), 0, s, m, tv);
+    return hipGetLastError();
+}
+
+hipError_t gpu_scene_slots(const DeviceMeshIn& m, const float* tv, const uint32_t* slot2tri, float4* tris,
+                           float4* snrm, float* tc, int32_t* orig2slot, hipStream_t s) {
+    if (m.ntri == 0) return hipSuccess;
+    hipLaunchKernelGGL(scene_slots_kernel, dim3(blocks(m.ntri)), dim3(kBlock), 0, s, m, tv, slot2tri, tris, snrm,
+                       tc, orig2slot);
+    return hipGetLastError();
+}
+
+}  // namespace spt

@@ -23,10 +23,11 @@ SPT_FLAG_FUSED = 4
 SPT_FLAG_WAVEFRONT = 8
 SPT_FLAG_TIMING_ALL = 16
 PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
+SPT_BUILD_AUTO, SPT_BUILD_HOST_SAH, SPT_BUILD_GPU_PLOC = 0, 1, 2
 
 # Every function include/spt.h declares (the CPU test checks they are exported).
 EXPORTED = [
-    "spt_init", "spt_scene_create", "spt_scene_set_albedo", "spt_scene_set_emission", "spt_scene_get_stats",
+    "spt_init", "spt_scene_create", "spt_scene_create_ex", "spt_scene_set_albedo", "spt_scene_set_emission", "spt_scene_get_stats",
     "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
     "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write",
@@ -85,7 +86,7 @@ class RenderStats(ctypes.Structure):
 
 class SceneStats(ctypes.Structure):
     _fields_ = [("ntri", c_uint64), ("nodes", c_uint64), ("leaves", c_uint64),
-                ("max_depth", c_uint32), ("max_leaf", c_uint32), ("bvh_width", c_uint32), ("reserved", c_uint32),
+                ("max_depth", c_uint32), ("max_leaf", c_uint32), ("bvh_width", c_uint32), ("builder", c_uint32),
                 ("device_bytes", c_uint64),
                 ("build_ms", c_double), ("sah_cost", c_double)]
 
@@ -115,6 +116,7 @@ def _load() -> ctypes.CDLL:
     sig = {
         "spt_init": (i32, [i32]),
         "spt_scene_create": (i32, [vp, vp, u64, u64, vp, vp, u64, vp, vp, u64, vp, POINTER(vp)]),
+        "spt_scene_create_ex": (i32, [vp, vp, u64, u64, vp, vp, u64, vp, vp, u64, vp, u32, POINTER(vp)]),
         "spt_scene_set_albedo": (i32, [vp, vp, u32]),
         "spt_scene_set_emission": (i32, [vp, vp, u32]),
         "spt_scene_get_stats": (i32, [vp, POINTER(SceneStats)]),

@@ -101,7 +101,8 @@ class HipBackend:
 
     # optix_backend.h:283-364 (arrays are host arrays here; the BVH is built on the host)
     def set_triangles_soup(self, position_triplets, positions, shading_normal_triplets=None, shading_normals=None,
-                           texcoord_triplets=None, texcoords=None, material_ids=None) -> None:
+                           texcoord_triplets=None, texcoords=None, material_ids=None, build: int = 0) -> None:
+        """build: _lib.SPT_BUILD_AUTO / SPT_BUILD_HOST_SAH / SPT_BUILD_GPU_PLOC."""
         if self.device is None:
             self.init(0)
         pt = np.ascontiguousarray(np.asarray(position_triplets, dtype=np.int32).reshape(-1))
@@ -118,11 +119,11 @@ class HipBackend:
         if self._scene.value:
             lib.spt_scene_destroy(self._scene)
             self._scene = ctypes.c_void_p()
-        check(lib.spt_scene_create(
+        check(lib.spt_scene_create_ex(
             _host_ptr(pt), _host_ptr(pos), pos.size // 3, ntri,
             _host_ptr(nt), _host_ptr(nrm), 0 if nrm is None else nrm.size // 3,
             _host_ptr(tt), _host_ptr(tc), 0 if tc is None else tc.size // 2,
-            _host_ptr(mat), ctypes.byref(self._scene)), "spt_scene_create")
+            _host_ptr(mat), build, ctypes.byref(self._scene)), "spt_scene_create")
         st = SceneStats()
         check(lib.spt_scene_get_stats(self._scene, ctypes.byref(st)), "spt_scene_get_stats")
         self.stats = st.as_dict()
@@ -245,11 +246,11 @@ class Scene:
     def add_arrays(self, mesh: dict) -> None:
         self.mesh = mesh
 
-    def commit(self, device: int = 0) -> None:             # main.cpp:312-318
+    def commit(self, device: int = 0, build: int = 0) -> None:  # main.cpp:312-318
         m = self.mesh
         self.backend.init(device)
         self.backend.set_triangles_soup(m["pos_tri"], m["pos"], m.get("nrm_tri"), m.get("nrm"), m.get("tc_tri"),
-                                        m.get("tc"), m.get("mat_id"))
+                                        m.get("tc"), m.get("mat_id"), build=build)
         if m.get("albedo") is not None:
             self.backend.set_albedo(m["albedo"])
         if m.get("emission") is not None:

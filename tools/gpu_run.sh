@@ -27,6 +27,9 @@ for s in "$@"; do
     tests) run tests 900 python -m pytest tests -m gpu -q -x ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
     tests2) run tests2 900 env SPT_BVH=2 python -m pytest tests -m gpu -q -x ;;
+    testsgb) run testsgb 900 env SPT_BUILD=gpu python -m pytest tests -m gpu -q -x ;;
+    bench4gq) run bench4gq 600 env SPT_BUILD=gpu python bench.py --config 4 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench1gq) run bench1gq 600 env SPT_BUILD=gpu python bench.py --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench2|bench3|bench4) run $s 600 python bench.py --config ${s#bench} --steps 2 --warmup 1 ;;
