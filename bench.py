@@ -78,8 +78,8 @@ def workload(args, scenes):
     smallpt mode (config 2): Kd albedo, Ke emitters, black sky, roulette from
     cast 5, smallpt's camera; otherwise the reference's semantics (albedo 1,
     sky 1, main.cpp:383 camera)."""
-    if args.scene == "city_synth":  # 10M triangles: arrays, not a 600 MB OBJ
-        return scenes.city_synth(10_000_000), dict(camera=scenes.city_camera()), None, None
+    if args.scene == "city_synth":  # 10M triangles through the pbrt-v3 reader (San Miguel's format), PLY meshes
+        return scenes.scene_pbrt("city_synth"), {}, None, None
     src = scenes.scene_obj(args.scene)
     if not args.smallpt:
         return src, {}, None, None
@@ -150,6 +150,8 @@ def main():
     scene.commit(local)
     t_commit = time.perf_counter() - t_commit
     mesh = scene.mesh
+    if scene.pbrt_info and scene.pbrt_info["camera"]:  # the .pbrt file's camera
+        kw = dict(kw, camera=scene.pbrt_info["camera"])
     if alb:
         alb, emi = scenes.smallpt_materials(mesh)
         scene.backend.set_albedo(alb)

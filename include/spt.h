@@ -228,6 +228,27 @@ const char* spt_version(void);
 spt_status spt_obj_load(const char* path, spt_mesh* out);
 void spt_mesh_free(spt_mesh* mesh);
 
+/* pbrt-v3 scene reader (the reference's pbrt-parser dependency, .gitmodules:7-9,
+ * CMakeLists.txt:57-61): triangle meshes ("trianglemesh",
+ * "plymesh"), transforms, attribute scopes, object instances (flattened),
+ * materials' diffuse Kd, diffuse area lights (emission), the perspective
+ * camera, film size and a constant infinite light.  Same spt_mesh as
+ * spt_obj_load (material 0 = default, shapes get their material + 1). */
+typedef struct spt_pbrt_info {
+    uint32_t has_camera;        /* a Camera directive was seen */
+    spt_camera camera;          /* look_from/at/up from the CTM at Camera; fov_y (radians) from "fov"
+                                   (pbrt's fov spans the shorter image axis) */
+    float fov_deg;              /* "float fov" as written (default 90) */
+    uint32_t xres, yres;        /* Film "xresolution" / "yresolution" (default 640 x 480) */
+    uint32_t has_env;           /* LightSource "infinite" seen */
+    float env[3];               /*   its radiance ("rgb L" x "scale") */
+    uint64_t shapes;            /* triangle shapes loaded (instanced ones once per definition) */
+    uint64_t shapes_skipped;    /* other shape types (sphere, curve, ...) */
+    uint64_t instances;         /* ObjectInstance directives flattened */
+} spt_pbrt_info;
+
+spt_status spt_pbrt_load(const char* path, spt_mesh* out, spt_pbrt_info* info);
+
 /* Fimage::save_pfm (fimage.h:33-58): planar R, G, B → interleaved,
  * rows bottom-up, scale -1 (little endian). */
 spt_status spt_pfm_write(const char* path, const float* r, const float* g, const float* b,

@@ -16,6 +16,7 @@
 #include "../../include/spt.h"
 #include "bvh_build.h"
 #include "gpu_build.h"
+#include "host_error.h"
 #include "spt_internal.h"
 
 using namespace spt;
@@ -334,6 +335,16 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
 }
 
 }  // namespace
+
+spt_status spt_set_error(spt_status code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
 
 extern "C" {
 

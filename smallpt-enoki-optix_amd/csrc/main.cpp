@@ -1,9 +1,10 @@
 // main.cpp — C++ host driver mirroring the reference's main() (main.cpp:354-446):
-// load an OBJ, commit the scene, render, normalise, read back, write a PFM,
-// print the wall time.  Every constant defaults to the reference's; flags
-// override them.
+// load an OBJ (or a pbrt-v3 scene), commit the scene, render, normalise, read
+// back, write a PFM, print the wall time.  Every constant defaults to the
+// reference's; a .pbrt file's camera, film size and infinite light replace
+// them, and flags override both.
 //
-//   spt_render_cli [scene.obj] [-w W] [-h H] [-s spp] [-d casts] [-o out.pfm]
+//   spt_render_cli [scene.obj|scene.pbrt] [-w W] [-h H] [-s spp] [-d casts] [-o out.pfm]
 //                  [--wavefront paths] [--rr depth] [--rng-x-first] [--device N]
 #include <hip/hip_runtime.h>
 
@@ -22,14 +23,15 @@ int main(int argc, char** argv) {
     int device = 0;
     spt_render_params p;
     spt_default_params(&p);            // 512 x 512, 100 spp, 2 casts (main.cpp:357-361)
+    bool set_w = false, set_h = false;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() -> const char* {
             if (i + 1 >= argc) { std::cerr << "missing value for " << a << "\n"; std::exit(2); }
             return argv[++i];
         };
-        if (a == "-w") p.width = (uint32_t)std::atoi(next());
-        else if (a == "-h") p.height = (uint32_t)std::atoi(next());
+        if (a == "-w") { p.width = (uint32_t)std::atoi(next()); set_w = true; }
+        else if (a == "-h") { p.height = (uint32_t)std::atoi(next()); set_h = true; }
         else if (a == "-s") p.spp = (uint32_t)std::atoi(next());
         else if (a == "-d") p.max_depth = (uint32_t)std::atoi(next());
         else if (a == "-o") out = next();
@@ -44,6 +46,14 @@ int main(int argc, char** argv) {
         spt::Scene scene;
         scene.add_triangle_mesh(obj);  // main.cpp:365
         scene.commit(device);          // main.cpp:366
+        const spt_pbrt_info& pi = scene.pbrt_info();
+        if (pi.has_camera) {
+            p.camera = pi.camera;
+            if (!set_w) p.width = pi.xres;
+            if (!set_h) p.height = pi.yres;
+        }
+        if (pi.has_env)
+            for (int c = 0; c < 3; c++) p.env[c] = pi.env[c];
         const size_t npx = (size_t)p.width * p.height;
         float* film = nullptr;
         if (hipMalloc((void**)&film, sizeof(float) * 3 * npx) != hipSuccess) throw std::runtime_error("hipMalloc film");

@@ -16,9 +16,19 @@ inline void check(spt_status s, const char* what) {
     if (s != SPT_OK) throw std::runtime_error(std::string(what) + " failed (" + std::to_string(s) + "): " + spt_last_error());
 }
 
+inline bool ends_with(const std::string& s, const char* suffix) {
+    const size_t n = std::char_traits<char>::length(suffix);
+    return s.size() >= n && s.compare(s.size() - n, n, suffix) == 0;
+}
+
+// An OBJ (main.cpp:141-251) or a pbrt-v3 scene (the pbrt-parser path), by extension.
 struct Mesh {
     spt_mesh m{};
-    explicit Mesh(const std::string& path) { check(spt_obj_load(path.c_str(), &m), "spt_obj_load"); }
+    spt_pbrt_info pbrt{};
+    explicit Mesh(const std::string& path) {
+        if (ends_with(path, ".pbrt")) check(spt_pbrt_load(path.c_str(), &m, &pbrt), "spt_pbrt_load");
+        else check(spt_obj_load(path.c_str(), &m), "spt_obj_load");
+    }
     ~Mesh() { spt_mesh_free(&m); }
     Mesh(const Mesh&) = delete;
     Mesh& operator=(const Mesh&) = delete;
@@ -33,7 +43,7 @@ class Scene {
     Scene(const Scene&) = delete;
     Scene& operator=(const Scene&) = delete;
 
-    void add_triangle_mesh(const std::string& obj_path) { mesh_.reset(new Mesh(obj_path)); }  // main.cpp:288
+    void add_triangle_mesh(const std::string& path) { mesh_.reset(new Mesh(path)); }  // main.cpp:288
     void commit(int device = 0) {                                                            // main.cpp:312
         if (!mesh_) throw std::runtime_error("Scene::commit: no mesh added");
         check(spt_init(device), "spt_init");
@@ -47,6 +57,7 @@ class Scene {
     }
     spt_scene handle() const { return scene_; }
     const spt_mesh& mesh() const { return mesh_->m; }
+    const spt_pbrt_info& pbrt_info() const { return mesh_->pbrt; }
 
   private:
     std::unique_ptr<Mesh> mesh_;

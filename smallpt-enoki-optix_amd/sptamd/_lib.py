@@ -30,7 +30,7 @@ EXPORTED = [
     "spt_init", "spt_scene_create", "spt_scene_create_ex", "spt_scene_set_albedo", "spt_scene_set_emission", "spt_scene_get_stats",
     "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
     "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
-    "spt_obj_load", "spt_mesh_free", "spt_pfm_write",
+    "spt_obj_load", "spt_mesh_free", "spt_pfm_write", "spt_pbrt_load",
 ]
 
 
@@ -102,6 +102,12 @@ class Mesh(ctypes.Structure):
                 ("ke", POINTER(c_float))]
 
 
+class PbrtInfo(ctypes.Structure):
+    _fields_ = [("has_camera", c_uint32), ("camera", Camera), ("fov_deg", c_float), ("xres", c_uint32),
+                ("yres", c_uint32), ("has_env", c_uint32), ("env", c_float * 3), ("shapes", c_uint64),
+                ("shapes_skipped", c_uint64), ("instances", c_uint64)]
+
+
 def _load() -> ctypes.CDLL:
     # torch ships its own HIP runtime (SONAME libamdhip64.so.7).  Load it first
     # so libspt.so binds to that one copy: loading libspt.so first would map the
@@ -130,6 +136,7 @@ def _load() -> ctypes.CDLL:
         "spt_version": (c_char_p, []),
         "spt_obj_load": (i32, [c_char_p, POINTER(Mesh)]),
         "spt_mesh_free": (None, [POINTER(Mesh)]),
+        "spt_pbrt_load": (i32, [c_char_p, POINTER(Mesh), POINTER(PbrtInfo)]),
         "spt_pfm_write": (i32, [c_char_p, vp, vp, vp, u32, u32]),
     }
     for name, (res, args) in sig.items():

@@ -238,10 +238,16 @@ class Scene:
     def __init__(self):
         self.backend = HipBackend()
         self.mesh = None
+        self.pbrt_info: Optional[dict] = None
 
-    def add_triangle_mesh(self, obj_path: str) -> None:   # main.cpp:288-310
-        from .scenes import load_obj
-        self.mesh = load_obj(obj_path)
+    def add_triangle_mesh(self, path: str) -> None:       # main.cpp:288-310
+        """An OBJ (load_meshes) or, by extension, a pbrt-v3 scene; for .pbrt
+        the file's camera / film / infinite light land in self.pbrt_info."""
+        from .scenes import load_obj, load_pbrt
+        if path.endswith(".pbrt"):
+            self.mesh, self.pbrt_info = load_pbrt(path)
+        else:
+            self.mesh = load_obj(path)
 
     def add_arrays(self, mesh: dict) -> None:
         self.mesh = mesh

@@ -21,7 +21,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
-from typing import Dict, List
+from typing import Dict, List, Optional
 
 import numpy as np
 
@@ -314,28 +314,159 @@ def _np_copy(ptr, n, dtype):
     return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype).copy()
 
 
+def _mesh_from_c(m) -> Dict[str, np.ndarray]:
+    out = dict(
+        pos_tri=_np_copy(m.pos_tri, 3 * m.ntri, np.int32).reshape(-1, 3),
+        pos=_np_copy(m.pos, 3 * m.nvert, np.float32).reshape(-1, 3),
+        nrm_tri=_np_copy(m.nrm_tri, 3 * m.ntri, np.int32).reshape(-1, 3),
+        nrm=_np_copy(m.nrm, 3 * m.nnrm, np.float32).reshape(-1, 3),
+        tc_tri=_np_copy(m.tc_tri, 3 * m.ntri, np.int32).reshape(-1, 3),
+        tc=_np_copy(m.tc, 2 * m.ntc, np.float32).reshape(-1, 2),
+        mat_id=_np_copy(m.mat_id, m.ntri, np.int32),
+        kd=_np_copy(m.kd, 3 * m.nmat, np.float32).reshape(-1, 3),
+        ke=_np_copy(m.ke, 3 * m.nmat, np.float32).reshape(-1, 3),
+    )
+    if out["tc"].size == 0:
+        out["tc"] = None
+        out["tc_tri"] = None
+    return out
+
+
 def load_obj(path: str) -> Dict[str, np.ndarray]:
     """load_meshes (main.cpp:141-251) through the C ABI's OBJ reader."""
     m = _lib.Mesh()
     _lib.check(_lib.lib.spt_obj_load(path.encode(), ctypes.byref(m)), f"spt_obj_load({path})")
     try:
-        out = dict(
-            pos_tri=_np_copy(m.pos_tri, 3 * m.ntri, np.int32).reshape(-1, 3),
-            pos=_np_copy(m.pos, 3 * m.nvert, np.float32).reshape(-1, 3),
-            nrm_tri=_np_copy(m.nrm_tri, 3 * m.ntri, np.int32).reshape(-1, 3),
-            nrm=_np_copy(m.nrm, 3 * m.nnrm, np.float32).reshape(-1, 3),
-            tc_tri=_np_copy(m.tc_tri, 3 * m.ntri, np.int32).reshape(-1, 3),
-            tc=_np_copy(m.tc, 2 * m.ntc, np.float32).reshape(-1, 2),
-            mat_id=_np_copy(m.mat_id, m.ntri, np.int32),
-            kd=_np_copy(m.kd, 3 * m.nmat, np.float32).reshape(-1, 3),
-            ke=_np_copy(m.ke, 3 * m.nmat, np.float32).reshape(-1, 3),
-        )
+        return _mesh_from_c(m)
     finally:
         _lib.lib.spt_mesh_free(ctypes.byref(m))
-    if out["tc"].size == 0:
-        out["tc"] = None
-        out["tc_tri"] = None
-    return out
+
+
+def load_pbrt(path: str):
+    """pbrt-v3 scene through the C ABI's reader (spt_pbrt_load).  Returns
+    (mesh dict as load_obj's, info dict: camera (make_params form) or None,
+    xres, yres, env or None, shapes, shapes_skipped, instances)."""
+    m = _lib.Mesh()
+    info = _lib.PbrtInfo()
+    _lib.check(_lib.lib.spt_pbrt_load(path.encode(), ctypes.byref(m), ctypes.byref(info)), f"spt_pbrt_load({path})")
+    try:
+        mesh = _mesh_from_c(m)
+    finally:
+        _lib.lib.spt_mesh_free(ctypes.byref(m))
+    c = info.camera
+    cam = dict(look_from=tuple(c.look_from), look_at=tuple(c.look_at), up=tuple(c.up), lens_radius=c.lens_radius,
+               focal_dist=c.focal_dist, fov_y=c.fov_y, film_size_y=c.film_size_y) if info.has_camera else None
+    return mesh, dict(camera=cam, fov_deg=info.fov_deg, xres=info.xres, yres=info.yres,
+                      env=tuple(info.env) if info.has_env else None, shapes=info.shapes,
+                      shapes_skipped=info.shapes_skipped, instances=info.instances)
+
+
+def _write_ply(path: str, pos: np.ndarray, nrm: Optional[np.ndarray], tris: np.ndarray, binary: bool = True) -> None:
+    """Triangle PLY: float x y z (nx ny nz), uchar/int vertex_indices lists."""
+    nv, nt = len(pos), len(tris)
+    props = ["x", "y", "z"] + (["nx", "ny", "nz"] if nrm is not None else [])
+    hdr = ["ply", "format binary_little_endian 1.0" if binary else "format ascii 1.0",
+           f"element vertex {nv}"] + [f"property float {p}" for p in props] + [
+           f"element face {nt}", "property list uchar int vertex_indices", "end_header"]
+    verts = np.ascontiguousarray(np.hstack([pos, nrm]) if nrm is not None else pos, dtype="<f4")
+    with open(path, "wb") as f:
+        f.write(("\n".join(hdr) + "\n").encode())
+        if binary:
+            f.write(verts.tobytes())
+            face = np.zeros(nt, dtype=[("n", "u1"), ("i", "<i4", (3,))])
+            face["n"] = 3
+            face["i"] = tris
+            f.write(face.tobytes())
+        else:
+            for v in verts:
+                f.write((" ".join(repr(float(x)) for x in v) + "\n").encode())
+            for t in tris:
+                f.write(f"3 {t[0]} {t[1]} {t[2]}\n".encode())
+
+
+def write_pbrt(path: str, mesh: Dict[str, np.ndarray], camera: Optional[dict] = None, width: int = 1024,
+               height: int = 1024, binary: bool = True) -> None:
+    """Write mesh as a pbrt-v3 scene: one "plymesh" per run of equal material
+    (triangle order kept), named matte materials with the mesh's Kd, diffuse
+    area lights for its Ke, LookAt + perspective camera."""
+    import math
+    base = os.path.splitext(path)[0]
+    stem = os.path.basename(base)
+    pos = np.asarray(mesh["pos"], np.float32).reshape(-1, 3)
+    pt = np.asarray(mesh["pos_tri"], np.int64).reshape(-1, 3)
+    nrm = mesh.get("nrm")
+    nt = mesh.get("nrm_tri")
+    has_n = nrm is not None and nt is not None and len(nrm) > 0
+    if has_n:
+        nrm = np.asarray(nrm, np.float32).reshape(-1, 3)
+        nt = np.asarray(nt, np.int64).reshape(-1, 3)
+        has_n = bool(np.all(nt >= 0))
+    mat = np.asarray(mesh.get("mat_id", np.zeros(len(pt), np.int32)), np.int64)
+    kd = np.asarray(mesh.get("kd", np.ones((1, 3))), np.float32).reshape(-1, 3)
+    ke = mesh.get("ke")
+    ke = np.zeros_like(kd) if ke is None else np.asarray(ke, np.float32).reshape(-1, 3)
+    cam = camera or dict(look_from=(0.0, 3.03, 5.0), look_at=(0.0, 0.03, 0.0), up=(0.0, 1.0, 0.0),
+                         fov_y=40.0 / 180.0 * math.pi)
+    fov = float(cam["fov_y"]) * 180.0 / math.pi
+    if width < height:  # pbrt's fov spans the shorter axis
+        fov = 2.0 * math.degrees(math.atan(math.tan(0.5 * float(cam["fov_y"])) * width / height))
+    lines = ["# written by sptamd.scenes.write_pbrt",
+             "LookAt " + " ".join(f"{float(x)!r}" for x in (*cam["look_from"], *cam["look_at"], *cam["up"])),
+             f'Camera "perspective" "float fov" [ {fov!r} ]',
+             f'Film "image" "integer xresolution" [ {width} ] "integer yresolution" [ {height} ]',
+             "WorldBegin"]
+    for i in range(1, len(kd)):
+        lines.append(f'MakeNamedMaterial "m{i}" "string type" "matte" '
+                     f'"rgb Kd" [ {float(kd[i][0])!r} {float(kd[i][1])!r} {float(kd[i][2])!r} ]')
+    change = np.flatnonzero(mat[1:] != mat[:-1]) + 1
+    starts = np.concatenate([[0], change]).astype(np.int64)
+    ends = np.concatenate([change, [len(mat)]]).astype(np.int64)
+    for k, (s, e) in enumerate(zip(starts.tolist(), ends.tolist())):
+        m = int(mat[s]) if len(mat) else 0
+        # per-vertex (position, normal) pairs of this run
+        if has_n:  # unique (position, normal) pairs, as one int64 key each
+            key = pt[s:e].reshape(-1) * np.int64(len(nrm)) + nt[s:e].reshape(-1)
+            uniq, inv = np.unique(key, return_inverse=True)
+            vp, vn = pos[uniq // len(nrm)], nrm[uniq % len(nrm)]
+        else:
+            uniq, inv = np.unique(pt[s:e].reshape(-1), return_inverse=True)
+            vp, vn = pos[uniq], None
+        ply = f"{stem}_{k}.ply"
+        _write_ply(os.path.join(os.path.dirname(path) or ".", ply), vp, vn, inv.reshape(-1, 3).astype(np.int32),
+                   binary=binary)
+        lines.append("AttributeBegin")
+        if m > 0:
+            lines.append(f'  NamedMaterial "m{m}"')
+            if m < len(ke) and np.any(ke[m] != 0):
+                lines.append(f'  AreaLightSource "diffuse" "rgb L" '
+                             f'[ {float(ke[m][0])!r} {float(ke[m][1])!r} {float(ke[m][2])!r} ]')
+        lines.append(f'  Shape "plymesh" "string filename" "{ply}"')
+        lines.append("AttributeEnd")
+    lines.append("WorldEnd")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def scene_pbrt(name: str, detail: float = 1.0) -> str:
+    """Path of a generated pbrt-v3 scene (+ PLY files), generated once into
+    build/scenes/.  city_synth: detail x 10M triangles, 1920 x 1080 film."""
+    d = os.path.join(SCENE_DIR, f"{name}_d{detail:g}_pbrt")
+    path = os.path.join(d, f"{name}.pbrt")
+    if not os.path.exists(path):
+        tmp = d + f".tmp{os.getpid()}"
+        os.makedirs(tmp, exist_ok=True)
+        out = os.path.join(tmp, f"{name}.pbrt")
+        if name == "city_synth":
+            write_pbrt(out, city_synth(int(10_000_000 * detail)), camera=city_camera(), width=1920, height=1080)
+        else:
+            gen = {"mitsuba_synth": mitsuba_synth, "cornell_spheres": cornell_spheres}[name]
+            write_pbrt(out, gen(detail), camera=cornell_camera() if name == "cornell_spheres" else None)
+        try:
+            os.replace(tmp, d)
+        except OSError:  # another process won
+            import shutil
+            shutil.rmtree(tmp, ignore_errors=True)
+    return path
 
 
 SCENE_DIR = os.path.join(_lib.REPO_ROOT, "build", "scenes")
