@@ -120,6 +120,7 @@ typedef struct spt_render_stats {
     uint32_t fused;             /* 1: the fused pipeline ran, 0: the wavefront */
     double isect_busy_ms;       /* SPT_FLAG_TIMING: union of the isect launch intervals
                                    (launches on the K streams overlap; isect_ms sums them) */
+    uint64_t isect_max_stack;   /* SPT_FLAG_TRAVERSAL_STATS: deepest LDS stack entry used */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

@@ -98,8 +98,7 @@ struct Counters {
 // Render-wide device statistics.
 struct Stats {
     unsigned long long stats[3];  // casts, continuations, camera rays started
-    unsigned long long trav[4];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps
-    unsigned long long pad;
+    unsigned long long trav[5];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps, max stack
 };
 
 constexpr int kMaxStreams = 4;
@@ -261,6 +260,16 @@ spt_status get_event(Workspace& ws, size_t idx, hipEvent_t* out) {
     return SPT_OK;
 }
 
+// LDS stack entries per lane for a BVH8 of `depth` node levels (root = 1).
+// Tracer8 pushes the group of node X (level L) only when descending into one
+// of X's inner children (level L + 1 <= depth), and the stack then holds one
+// group per node on the path root..X: at most depth - 1 entries.  A tight
+// stack is LDS, and LDS sets the occupancy (env SPT_STACK_SLACK adds entries).
+uint32_t bvh8_stack_entries(uint32_t depth) {
+    static const uint32_t slack = env_u32("SPT_STACK_SLACK", 0, 0, 64);
+    return std::max<uint32_t>(1, depth > 1 ? depth - 1 + slack : 1 + slack);
+}
+
 // Triangle count from which SPT_BUILD_AUTO builds on the GPU.
 constexpr uint64_t kGpuBuildAutoTris = 2000000;
 
@@ -293,7 +302,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     spt_scene_t* sc = new spt_scene_t();
     (void)hipGetDevice(&sc->device);
     sc->ntri = ntri;
-    sc->stack_depth = g.depth + 1;
+    sc->stack_depth = bvh8_stack_entries(g.depth);
     sc->nodes8 = (uint4*)g.nodes8;
     auto bail = [&](hipError_t e) {
         (void)hipFree(g.slot2tri);
@@ -493,7 +502,7 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
     spt_scene_t* sc = new spt_scene_t();
     (void)hipGetDevice(&sc->device);
     sc->ntri = ntri;
-    sc->stack_depth = std::max<uint32_t>(1, (use8 ? bvh8.depth : bvh.max_depth) + 1);
+    sc->stack_depth = use8 ? bvh8_stack_entries(bvh8.depth) : std::max<uint32_t>(1, bvh.max_depth + 1);
     const float one[3] = {1.0f, 1.0f, 1.0f};
     spt_status us = SPT_OK;
     if (use8) {
@@ -932,7 +941,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
              })))
             return st;
     }
-    unsigned long long hstats[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long hstats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(hstats, ws.stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
@@ -943,6 +952,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     rs.isect_tris = hstats[4];
     rs.isect_lane_steps = hstats[5];
     rs.isect_wave_steps = hstats[6];
+    rs.isect_max_stack = hstats[7];
     if (timing) {
         uint64_t nis = 0;
         std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin

@@ -21,12 +21,14 @@ struct NoStats {
     __device__ void node() {}
     __device__ void tri() {}
     __device__ void step() {}
+    __device__ void push(uint32_t) {}
 };
 struct TravStats {
-    uint32_t nodes = 0, tris = 0, steps = 0;
+    uint32_t nodes = 0, tris = 0, steps = 0, max_sp = 0;
     __device__ void node() { nodes++; }
     __device__ void tri() { tris++; }
     __device__ void step() { steps++; }
+    __device__ void push(uint32_t sp) { max_sp = max(max_sp, sp); }
 };
 
 // Stack-based BVH2 traversal, near child first, stack in LDS at
@@ -91,6 +93,7 @@ struct Tracer {
                 const bool swp = tn1 < tn0;
                 stk[sp * kIsectBlock] = (uint32_t)(swp ? ch0 : ch1);
                 sp++;
+                stats.push(sp);
                 node = swp ? ch1 : ch0;
                 return false;
             }
@@ -251,6 +254,7 @@ struct Tracer8 {
             stk[(2 * sp) * kIsectBlock] = nbase;
             stk[(2 * sp + 1) * kIsectBlock] = nhits;
             sp++;
+            stats.push(sp);
         }
         visit(sc, child);
         return false;
@@ -276,8 +280,12 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
 // quarter from the launch-wide counter *a.next, which evens out the tail.
 // The last cast of a path only needs a yes/no answer (a miss is the only thing
 // that contributes, main.cpp:407), so it runs as an any-hit query.
+#ifndef SPT_ISECT_WAVES
+#define SPT_ISECT_WAVES 1
+#endif
 template <typename Tr, bool kStats>
-__global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs a) {
+__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_ISECT_WAVES, 8)))
+void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
     uint32_t* stk = lds_stack + threadIdx.x;
     const uint32_t n = *a.count;
@@ -338,6 +346,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_queue_kernel(IsectQueueArgs
         atomicAdd(&a.trav_stats[1], (unsigned long long)st.tris);
         atomicAdd(&a.trav_stats[2], (unsigned long long)st.steps);
         if ((threadIdx.x & 63u) == 0) atomicAdd(&a.trav_stats[3], (unsigned long long)wave_steps);
+        atomicMax(&a.trav_stats[4], (unsigned long long)st.max_sp);
     }
 }
 

@@ -78,7 +78,8 @@ class RenderStats(ctypes.Structure):
                 ("resolve_ms", c_double), ("total_ms", c_double),
                 ("isect_nodes", c_uint64), ("isect_tris", c_uint64), ("isect_lane_steps", c_uint64),
                 ("isect_wave_steps", c_uint64), ("isect_launches", c_uint64), ("streams", c_uint32),
-                ("fused", c_uint32), ("isect_busy_ms", c_double)]
+                ("fused", c_uint32), ("isect_busy_ms", c_double),
+                ("isect_max_stack", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -46,7 +46,8 @@ def main():
                "nodes_per_ray": round(ss["isect_nodes"] / casts, 2),
                "tris_per_ray": round(ss["isect_tris"] / casts, 2),
                "steps_per_ray": round(ss["isect_lane_steps"] / casts, 2),
-               "simd_eff": round(ss["isect_lane_steps"] / (64.0 * ss["isect_wave_steps"]), 3)}
+               "simd_eff": round(ss["isect_lane_steps"] / (64.0 * ss["isect_wave_steps"]), 3),
+               "max_stack": ss["isect_max_stack"]}
         print(json.dumps(rec), flush=True)
 
 
