@@ -16,6 +16,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <utility>
+#include <vector>
 
 #include "gpu_build.h"
 #include "spt_internal.h"
@@ -229,6 +232,64 @@ __global__ __launch_bounds__(kBlock) void sah_kernel(const float4* __restrict__ 
 }
 
 // ---------------------------------------------------------------- collapse
+// SAH-optimal collapse (Ylitie et al. 2017 §3.1, as bvh8_build.cpp mode 3),
+// bottom-up over the PLOC nodes one merge iteration at a time (a node's
+// children were made in earlier iterations).  Per inner node: cost[i-1] =
+// least cost of the subtree as at most i BVH8 children (i = 1..8); take bit
+// i: that is cost[i-2] (i >= 2), bit 1: as a leaf (else a BVH8 node); split
+// 3 bits per i = 2..8: the left child's share of i slots.
+struct DpNode {
+    float cost[8];
+    uint32_t split;
+    uint32_t take;
+};
+constexpr float kCNode = 1.0f, kCPrim = 0.3f;
+
+__device__ __forceinline__ float dp_kid_cost(const DpNode* __restrict__ dp, const float4* __restrict__ lo,
+                                             const float4* __restrict__ hi, uint32_t ntri, uint32_t k, int i) {
+    return k < ntri ? 2.0f * half_area(lo[k], hi[k]) * kCPrim : dp[k - ntri].cost[i - 1];
+}
+
+__global__ __launch_bounds__(kBlock) void dp_kernel(const float4* __restrict__ lo, const float4* __restrict__ hi,
+                                                    const int2* __restrict__ kids2, const uint32_t* __restrict__ ntris,
+                                                    uint32_t ntri, uint32_t first, uint32_t count,
+                                                    DpNode* __restrict__ dp) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= count) return;
+    const uint32_t n = first + j;
+    const int2 c = kids2[n];
+    const uint32_t l = (uint32_t)c.x, r = (uint32_t)c.y;
+    float cl[9], cr[9];
+    for (int i = 1; i <= 8; i++) {
+        cl[i] = dp_kid_cost(dp, lo, hi, ntri, l, i);
+        cr[i] = dp_kid_cost(dp, lo, hi, ntri, r, i);
+    }
+    float D[9];
+    uint32_t split = 0;
+    for (int i = 2; i <= 8; i++) {
+        D[i] = INFINITY;
+        uint32_t bs = 1;
+        for (int k = 1; k < i; k++) {
+            const float v = cl[k] + cr[i - k];
+            if (v < D[i]) { D[i] = v; bs = (uint32_t)k; }
+        }
+        split |= bs << (3 * (i - 2));
+    }
+    const float area = 2.0f * half_area(lo[n], hi[n]);
+    const float lc = ntris[n] <= kLeafMaxTris ? area * kCPrim * (float)ntris[n] : INFINITY;
+    const float ic = area * kCNode + D[8];
+    DpNode out;
+    out.cost[0] = fminf(lc, ic);
+    uint32_t take = lc <= ic ? 2u : 0u;
+    for (int i = 2; i <= 8; i++) {
+        if (out.cost[i - 2] <= D[i]) take |= 1u << i;
+        out.cost[i - 1] = fminf(out.cost[i - 2], D[i]);
+    }
+    out.split = split;
+    out.take = take;
+    dp[n - ntri] = out;
+}
+
 struct CollapseArgs {
     const float4* lo;
     const float4* hi;
@@ -237,16 +298,20 @@ struct CollapseArgs {
     uint32_t ntri;
     const uint32_t* queue;   // BVH2 node of each BVH8 node of this level (root-leaf: a leaf id)
     uint32_t count;
-    uint32_t* kids8;         // [count][8] chosen BVH2 children, 0xffffffff = empty
+    uint32_t* kids8;         // [count][8] chosen BVH2 children | kLeafKid, 0xffffffff = empty
     uint64_t* counts;        // inner << 32 | leaf triangles
+    const DpNode* dp;        // SAH-optimal decisions (null: greedy collapse)
 };
+
+constexpr uint32_t kLeafKid = 0x80000000u;  // kids8 flag: the child becomes a BVH8 leaf
 
 __device__ __forceinline__ bool leafable(const CollapseArgs& a, uint32_t node) {
     return node < a.ntri || a.ntris[node] <= kLeafMaxTris;
 }
 
-// Pass A: one thread per BVH8 node of the level; greedy collapse (open the
-// largest-area child that cannot be a leaf while fewer than 8 children).
+// Pass A: one thread per BVH8 node of the level: the DP's distribution of the
+// 8 slots (or the greedy collapse: open the largest-area child that cannot be
+// a leaf while fewer than 8 children).
 __global__ __launch_bounds__(kBlock) void collapse_pick_kernel(CollapseArgs a) {
     const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
     if (e >= a.count) return;
@@ -254,13 +319,32 @@ __global__ __launch_bounds__(kBlock) void collapse_pick_kernel(CollapseArgs a) {
     uint32_t k[8];
     uint32_t nk = 0;
     if (root < a.ntri) {  // single-triangle scene: the root is a leaf
-        k[nk++] = root;
+        k[nk++] = root | kLeafKid;
+    } else if (a.dp) {
+        // collect(element, slots), left child first, with an explicit stack
+        uint32_t sn[8], si[8], sp = 0;
+        const int2 c = a.kids2[root];
+        const uint32_t s8 = (a.dp[root - a.ntri].split >> 18) & 7u;
+        sn[sp] = (uint32_t)c.y; si[sp++] = 8u - s8;
+        sn[sp] = (uint32_t)c.x; si[sp++] = s8;
+        while (sp) {
+            const uint32_t x = sn[--sp];
+            uint32_t i = si[sp];
+            if (x < a.ntri) { k[nk++] = x | kLeafKid; continue; }
+            const DpNode& d = a.dp[x - a.ntri];
+            while (i > 1 && ((d.take >> i) & 1u)) i--;
+            if (i == 1) { k[nk++] = x | (((d.take >> 1) & 1u) ? kLeafKid : 0u); continue; }
+            const uint32_t s = (d.split >> (3 * (i - 2))) & 7u;
+            const int2 cc = a.kids2[x];
+            sn[sp] = (uint32_t)cc.y; si[sp++] = i - s;
+            sn[sp] = (uint32_t)cc.x; si[sp++] = s;
+        }
     } else {
         const int2 c = a.kids2[root];
         k[nk++] = (uint32_t)c.x;
         k[nk++] = (uint32_t)c.y;
     }
-    while (nk < 8) {
+    while (!a.dp && nk < 8 && root >= a.ntri) {
         int best = -1;
         float ba = -1.0f;
         for (uint32_t i = 0; i < nk; i++)
@@ -273,12 +357,15 @@ __global__ __launch_bounds__(kBlock) void collapse_pick_kernel(CollapseArgs a) {
         k[best] = (uint32_t)c.x;
         k[nk++] = (uint32_t)c.y;
     }
+    if (!a.dp)
+        for (uint32_t i = 0; i < nk; i++)
+            if (!(k[i] & kLeafKid) && leafable(a, k[i])) k[i] |= kLeafKid;
     uint32_t ninner = 0, nleaf = 0;
     for (uint32_t i = 0; i < 8; i++) {
         const uint32_t v = i < nk ? k[i] : 0xffffffffu;
         a.kids8[(size_t)e * 8 + i] = v;
         if (i < nk) {
-            if (leafable(a, v)) nleaf += a.ntris[v];
+            if (v & kLeafKid) nleaf += a.ntris[v & ~kLeafKid];
             else ninner++;
         }
     }
@@ -303,10 +390,12 @@ __global__ __launch_bounds__(kBlock) void collapse_emit_kernel(EmitArgs a) {
     const uint32_t e = blockIdx.x * kBlock + threadIdx.x;
     if (e >= a.c.count) return;
     uint32_t k[8];
-    uint32_t nk = 0;
+    uint32_t nk = 0, leafbits = 0;
     for (uint32_t i = 0; i < 8; i++) {
         const uint32_t v = a.c.kids8[(size_t)e * 8 + i];
-        if (v != 0xffffffffu) k[nk++] = v;
+        if (v == 0xffffffffu) continue;
+        if (v & kLeafKid) leafbits |= 1u << nk;
+        k[nk++] = v & ~kLeafKid;
     }
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (uint32_t i = 0; i < nk; i++) {
@@ -383,7 +472,7 @@ __global__ __launch_bounds__(kBlock) void collapse_emit_kernel(EmitArgs a) {
             q[ax][s] = (uint8_t)ql;
             q[3 + ax][s] = (uint8_t)qh;
         }
-        if (!leafable(a.c, node)) {
+        if (!((leafbits >> kk) & 1u)) {
             imask |= 1u << s;
             meta[s] = (uint8_t)(0x20u | (24u + (uint32_t)s));
             a.next_queue[child_base - a.next_first + r] = node;
@@ -510,6 +599,7 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
     GB_TRY(tmp.get((char**)&scan_ws, scan_bytes));
     uint32_t n = ntri, cur = 0, node_base = ntri, iters = 0;
     uint64_t tot = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> made;  // inner nodes made per iteration (first, count)
     while (n > 1) {
         switch (radius) {
             case 8: hipLaunchKernelGGL(nn_kernel<8>, dim3(blocks(n)), dim3(kBlock), 0, s, clo[cur], chi[cur], n, nn); break;
@@ -529,6 +619,7 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
         GB_TRY(hipStreamSynchronize(s));
         const uint32_t merged = (uint32_t)(tot >> 32), kept = (uint32_t)(tot & 0xffffffffu);
         if (merged == 0) return hipErrorUnknown;  // cannot happen (see nn_kernel)
+        made.push_back({node_base, merged});
         node_base += merged;
         n = kept;
         cur = 1 - cur;
@@ -543,6 +634,18 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
     GB_TRY(hipStreamSynchronize(s));
     out->bvh2_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     out->ploc_iterations = iters;
+
+    // SAH-optimal collapse decisions, bottom-up by merge iteration (env
+    // SPT_GPU_COLLAPSE=greedy keeps the greedy collapse)
+    DpNode* dp = nullptr;
+    const char* gc = std::getenv("SPT_GPU_COLLAPSE");
+    if (!(gc && std::strcmp(gc, "greedy") == 0) && ntri > 1) {
+        GB_TRY(tmp.get(&dp, ntri - 1));
+        for (const auto& m : made)
+            hipLaunchKernelGGL(dp_kernel, dim3(blocks(m.second)), dim3(kBlock), 0, s, lo, hi, kids2, ntris, ntri,
+                               m.first, m.second, dp);
+        GB_TRY(hipGetLastError());
+    }
 
     // Collapse, level by level.  At most ntri BVH8 nodes (every node holds
     // at least two children or is the single root).
@@ -562,7 +665,7 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
     void* scan8_ws = nullptr;
     hipError_t err = tmp.get((char**)&scan8_ws, scan8_bytes);
     while (err == hipSuccess && count > 0) {
-        CollapseArgs c{lo, hi, kids2, ntris, ntri, queue[q], count, kids8, counts};
+        CollapseArgs c{lo, hi, kids2, ntris, ntri, queue[q], count, kids8, counts, dp};
         hipLaunchKernelGGL(collapse_pick_kernel, dim3(blocks(count)), dim3(kBlock), 0, s, c);
         if ((err = hipGetLastError())) break;
         if ((err = hipcub::DeviceScan::ExclusiveSum(scan8_ws, scan8_bytes, counts, scan, (int)count, s))) break;
