@@ -410,9 +410,17 @@ static inline int woop_test(const wray* r, const float* tv, float tmin, float tm
 }
 
 #define BOX_PAD 1.000001f
+/* Slab test over the closed box.  A direction component whose reciprocal is
+ * infinite (d = +-0 or denormal) makes the ray parallel to that slab pair: it
+ * is inside the slab for every t or never ((b - o) * inf would give NaN when
+ * the origin lies on a plane). */
 static inline int box_test(const wray* r, const onode* nd, float tmin, float tmax) {
     float tn = tmin, tf = tmax;
     for (int k = 0; k < 3; k++) {
+        if (isinf(r->inv[k])) {
+            if (r->o[k] < nd->bmin[k] || r->o[k] > nd->bmax[k]) return 0;
+            continue;
+        }
         float t0 = (nd->bmin[k] - r->o[k]) * r->inv[k];
         float t1 = (nd->bmax[k] - r->o[k]) * r->inv[k];
         float lo = fminf(t0, t1), hi = fmaxf(t0, t1) * BOX_PAD;
@@ -449,7 +457,9 @@ static void trace(const oscene* s, const wray* r, float tmin, float tmax, int cl
     stack[sp++] = 0;
     while (sp) {
         const onode* nd = &s->nodes[stack[--sp]];
-        if (!box_test(r, nd, tmin, h->t)) continue;
+        /* the current hit padded like the exit planes: boxes entered at the
+         * hit's t (ties at shared edges / vertices) are still visited */
+        if (!box_test(r, nd, tmin, h->t * BOX_PAD)) continue;
         if (nd->count) {
             for (int32_t i = 0; i < nd->count; i++) {
                 consider(s, r, s->prims[nd->left + i], tmin, h);

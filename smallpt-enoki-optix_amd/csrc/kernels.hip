@@ -39,6 +39,22 @@ struct TravStats {
 //
 // Resumable: step() advances one node or one leaf and returns true when the
 // ray is finished, so a persistent wave can swap finished lanes for new rays.
+// One slab of the BVH2 box test: the plane distances (p0 - o) / d, (p1 - o) / d
+// as t0, t1 (in either order).  A direction component with an infinite
+// reciprocal (d = +-0 or denormal) leaves the ray parallel to the slab: inside
+// it for every t (t0, t1 = -inf, +inf) or never (+inf, +inf) — the product
+// would be NaN for an origin on a plane.
+__device__ __forceinline__ void slab(float p0, float p1, float o, float inv, float& t0, float& t1) {
+    if (isinf(inv)) {
+        const bool in = o >= p0 && o <= p1;
+        t0 = in ? -INFINITY : INFINITY;
+        t1 = INFINITY;
+        return;
+    }
+    t0 = (p0 - o) * inv;
+    t1 = (p1 - o) * inv;
+}
+
 struct Tracer {
     WoopRay wr;
     V3 o;
@@ -76,18 +92,24 @@ struct Tracer {
             stats.node();
             const float4* np = sc.nodes + (size_t)node * 4;
             const float4 n0 = np[0], n1 = np[1], n2 = np[2], n3 = np[3];
-            const float a0 = (n0.x - o.x) * ix, a1 = (n0.y - o.x) * ix;
-            const float b0 = (n0.z - o.y) * iy, b1 = (n0.w - o.y) * iy;
-            const float c0 = (n2.x - o.z) * iz, c1 = (n2.y - o.z) * iz;
+            float a0, a1, b0, b1, c0, c1;
+            slab(n0.x, n0.y, o.x, ix, a0, a1);
+            slab(n0.z, n0.w, o.y, iy, b0, b1);
+            slab(n2.x, n2.y, o.z, iz, c0, c1);
             const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), tmin));
             const float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1)) * kBoxPad;
-            const float d0 = (n1.x - o.x) * ix, d1 = (n1.y - o.x) * ix;
-            const float e0 = (n1.z - o.y) * iy, e1 = (n1.w - o.y) * iy;
-            const float f0 = (n2.z - o.z) * iz, f1 = (n2.w - o.z) * iz;
+            float d0, d1, e0, e1, f0, f1;
+            slab(n1.x, n1.y, o.x, ix, d0, d1);
+            slab(n1.z, n1.w, o.y, iy, e0, e1);
+            slab(n2.z, n2.w, o.z, iz, f0, f1);
             const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fmaxf(fminf(f0, f1), tmin));
             const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1)) * kBoxPad;
-            const bool h0 = tn0 <= fminf(tf0, h.t);
-            const bool h1 = tn1 <= fminf(tf1, h.t);
+            // the current hit padded like the exit planes: a box entered at the
+            // hit's t (a tie at a shared edge or vertex) is still visited, so
+            // the smaller triangle id wins whatever the traversal order
+            const float th = h.t * kBoxPad;
+            const bool h0 = tn0 <= fminf(tf0, th);
+            const bool h1 = tn1 <= fminf(tf1, th);
             const int32_t ch0 = (int32_t)f2u(n3.x), ch1 = (int32_t)f2u(n3.y);
             if (h0 && h1) {
                 const bool swp = tn1 < tn0;

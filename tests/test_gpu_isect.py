@@ -166,3 +166,56 @@ def test_hit_info(backend, mesh, oracle_bvh):
     gn = gn / np.linalg.norm(gn, axis=0)
     np.testing.assert_allclose(hit.geometry_normal.cpu().numpy()[:, h], gn, atol=2e-5)
     np.testing.assert_array_equal(hit.material_id.cpu().numpy()[h], mesh["mat_id"][ids])
+
+
+def grid_mesh(n=16):
+    """n x n quads in the plane y = 0, two triangles each, sharing edges."""
+    xs = np.linspace(-1.0, 1.0, n + 1, dtype=np.float32)
+    gx, gz = np.meshgrid(xs, xs, indexing="ij")
+    pos = np.stack([gx.ravel(), np.zeros(gx.size, np.float32), gz.ravel()], 1)
+    i = np.arange(n)[:, None] * (n + 1) + np.arange(n)[None, :]
+    a, b, c, d = i, i + n + 1, i + n + 2, i + 1
+    tris = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+    return {"pos_tri": tris.astype(np.int32), "pos": pos}
+
+
+def test_watertight_shared_edges_and_vertices():
+    """Rays aimed exactly at shared edges and vertices of a triangle grid hit
+    (no cracks: the watertight test, SURVEY §7 hard part 3), with the oracle's
+    tie-broken triangle."""
+    m = grid_mesh(16)
+    b = sptamd.HipBackend()
+    b.init(0)
+    b.set_triangles_soup(m["pos_tri"], m["pos"])
+    pts = m["pos"][np.abs(m["pos"][:, 0]) < 0.99]
+    pts = pts[np.abs(pts[:, 2]) < 0.99]                              # interior vertices
+    mids = (m["pos"][m["pos_tri"][:, 0]] + m["pos"][m["pos_tri"][:, 2]]) * np.float32(0.5)  # diagonal midpoints
+    targets = np.concatenate([pts, mids]).astype(np.float32)
+    rng = np.random.default_rng(11)
+    o = (targets + rng.normal(size=targets.shape).astype(np.float32) * [0.3, 0.0, 0.3]).astype(np.float32)
+    o[:, 1] = rng.uniform(0.5, 3.0, size=len(o))
+    d = (targets - o).astype(np.float32).T.copy()
+    o = o.T.copy()
+    got = gpu_isect(b, o, d)
+    ref = O.OracleScene(m, use_bvh=False).intersect(o, d)
+    assert_hits_equal(got, ref)
+    assert (got[0] >= 0).mean() > 0.99
+
+
+def test_axis_aligned_and_degenerate_rays(backend, oracle_bvh):
+    """Direction components of +0, -0 and tiny magnitude (1/d = inf or huge),
+    zero-length and NaN directions: same answers as the oracle, no faults."""
+    o, d = random_rays(6000, 12)
+    n = o.shape[1]
+    d[0, 0::6] = 0.0
+    d[1, 1::6] = -0.0
+    d[2, 2::6] = 1e-30
+    d[:, 3::6] = 0.0                      # zero direction: misses
+    d[0, 4::6] = 0.0
+    d[2, 4::6] = 0.0                      # straight down/up the y axis
+    d[0, 5::6] = np.nan                   # NaN direction: misses
+    got = gpu_isect(backend, o, d)
+    ref = oracle_bvh.intersect(o, d)
+    assert_hits_equal(got, ref)
+    assert (got[0][3::6] == -1).all() and (got[0][5::6] == -1).all()
+    assert (got[0] >= 0).sum() > n // 10

@@ -265,3 +265,32 @@ def test_film_is_escape_fraction():
     counts = f[0] * np.float32(7)
     np.testing.assert_allclose(counts, np.round(counts), atol=1e-5)
     assert 0.0 < f.mean() < 1.0
+
+
+def test_bvh_ties_and_parallel_rays_equal_bruteforce():
+    """The oracle's BVH gives brute force's answer on rays aimed at shared
+    edges and vertices (t ties: the smaller triangle id must win whatever
+    box is entered first) and on rays parallel to slab planes with the
+    origin on a plane (d = +-0: 0 * inf would be NaN)."""
+    n = 16
+    xs = np.linspace(-1.0, 1.0, n + 1, dtype=np.float32)
+    gx, gz = np.meshgrid(xs, xs, indexing="ij")
+    pos = np.stack([gx.ravel(), np.zeros(gx.size, np.float32), gz.ravel()], 1)
+    i = np.arange(n)[:, None] * (n + 1) + np.arange(n)[None, :]
+    a, b, c, d = i, i + n + 1, i + n + 2, i + 1
+    tris = np.concatenate([np.stack([a, b, c], -1).reshape(-1, 3), np.stack([a, c, d], -1).reshape(-1, 3)])
+    m = {"pos_tri": tris.astype(np.int32), "pos": pos}
+    rng = np.random.default_rng(5)
+    targets = pos[rng.integers(0, len(pos), 3000)]
+    o = (targets + rng.normal(size=targets.shape).astype(np.float32) * np.float32([0.3, 0.0, 0.3]))
+    o[:, 1] = rng.uniform(0.5, 3.0, size=len(o))
+    o = o.astype(np.float32)
+    dd = (targets - o).astype(np.float32)
+    dd[::4, 0] = 0.0                        # parallel to the x slabs, origin on a grid plane
+    o[::4, 0] = targets[::4, 0]
+    o, dd = o.T.copy(), dd.T.copy()
+    bvh = O.OracleScene(m, use_bvh=True).intersect(o, dd)
+    brute = O.OracleScene(m, use_bvh=False).intersect(o, dd)
+    for x, y in zip(bvh, brute):
+        np.testing.assert_array_equal(x, y)
+    assert (brute[0] >= 0).mean() > 0.95
