@@ -177,7 +177,9 @@ struct Tracer8 {
         const float dx = fabsf(d.x) < kMinDir ? copysignf(kMinDir, d.x) : d.x;
         const float dy = fabsf(d.y) < kMinDir ? copysignf(kMinDir, d.y) : d.y;
         const float dz = fabsf(d.z) < kMinDir ? copysignf(kMinDir, d.z) : d.z;
-        ix = 1.0f / dx; iy = 1.0f / dy; iz = 1.0f / dz;
+        // hardware reciprocal (<= 1 ulp): the slab margins (kMarginRel) absorb
+        // it, and the triangle test keeps its own correctly rounded divides
+        ix = __builtin_amdgcn_rcpf(dx); iy = __builtin_amdgcn_rcpf(dy); iz = __builtin_amdgcn_rcpf(dz);
         const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
         oct_inv = oct ^ 7u;
         tmin = tmin_;
