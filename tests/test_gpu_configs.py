@@ -1,0 +1,79 @@
+"""BASELINE.json configs[2..4] at their full sizes on the GPU (configs[1] is
+tests/test_gpu_render.py::test_headline_config_properties): the whole image is
+rendered exactly as bench.py renders it, sampled rows are compared bit for bit
+with the CPU oracle, and size-independent properties are checked on the rest
+(finite, non-negative; with albedo 1 and sky 1 every value a multiple of
+1/spp in [0, 1])."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import sptamd
+from sptamd import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (the configs and their scene setup)
+
+pytestmark = pytest.mark.gpu
+
+
+def setup(config):
+    cfg = bench.CONFIGS[config]
+    src, kw, smallpt, _ = bench.workload(argparse.Namespace(scene=cfg["scene"], smallpt=cfg["smallpt"]), scenes)
+    s = sptamd.Scene()
+    if isinstance(src, str):
+        s.add_triangle_mesh(src)
+    else:
+        s.add_arrays(src)
+    s.commit(0)
+    if s.pbrt_info and s.pbrt_info["camera"]:
+        kw = dict(kw, camera=s.pbrt_info["camera"])
+    alb = emi = None
+    if smallpt:
+        alb, emi = scenes.smallpt_materials(s.mesh)
+        s.backend.set_albedo(alb)
+        s.backend.set_emission(emi)
+    return cfg, s, kw, alb, emi
+
+
+def run(config, rows):
+    cfg, s, kw, alb, emi = setup(config)
+    W, H, spp, D = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
+    film, st = s.render(sptamd.make_params(W, H, spp, D, **kw))
+    torch.cuda.synchronize()
+    got = film[:, rows, :].cpu().numpy()
+    whole = film
+    assert bool(torch.isfinite(whole).all()) and bool((whole >= 0).all())
+    osc = O.OracleScene(s.mesh, albedo=alb, emission=emi)
+    ref, casts = osc.render(O.reference_params(W, H, spp, D, **kw), rows=np.asarray(rows, np.int32),
+                            nthreads=16)
+    np.testing.assert_array_equal(got, ref)
+    assert st["paths"] == W * H * spp
+    return whole, st, spp
+
+
+def test_config2_cornell_full_size():
+    """1024^2 x 1024 spp, depth 10, Kd albedo, Ke light, roulette from cast 5."""
+    film, st, spp = run(2, [100, 700])
+    assert st["ray_casts"] > 4 * st["paths"]          # the compaction stress case
+    assert float(film.max()) > 0
+
+
+def test_config3_tiled_size_full():
+    """4096^2 x 256 spp, depth 8 (the per-GPU tile at N = 1)."""
+    film, st, spp = run(3, [2048])
+    f = film[:, ::64, :]
+    assert bool(((f * spp) == torch.round(f * spp)).all()) and bool((f <= 1).all())
+
+
+def test_config4_city_pbrt_full_size():
+    """10M triangles through the pbrt reader and the GPU builder, 1920x1080 x 64 spp."""
+    film, st, spp = run(4, [540])
+    f = film[:, ::32, :]
+    assert bool(((f * spp) == torch.round(f * spp)).all()) and bool((f <= 1).all())
