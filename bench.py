@@ -25,7 +25,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "isect_traffic.json")  # tools/pmc_traffic.py output
+PMC_JSON = os.path.join(ROOT, "profiles", "isect_pmc.json")  # tools/pmc_isect.sh output
+VALU_PEAK_G = 256 * 4 * 2.4 / 2  # wave64 VALU instr/s (G): 1024 SIMDs, 2 cycles each at 2.4 GHz (MI355X_MICROARCH.md)
 ISECT_BYTES_PER_CAST = 44      # ray 24 B + meta 4 B in, hit 16 B out
 FUSED_BYTES_PER_PATH = 12      # per-sample film RGB write
 
@@ -208,14 +209,17 @@ def main():
     value = paths / elapsed / 1e6
     if rank == 0:
         # roofline of the dominant kernel: algorithmic bytes per launch / average
-        # launch time (HIP events, rank 0's tile).  Wavefront: isect_queue_kernel,
-        # 44 B per ray cast.  Fused: render_fused_kernel, whose only HBM stream is
-        # the per-sample film write (12 B per path; rays stay in registers).
-        # The wavefront runs K sub-wavefronts on K streams, so isect launches
-        # overlap: `achieved` divides the bytes of all launches by the union of
-        # their intervals (the time the isect kernel occupies the chip), and
-        # `per_launch` is bytes per launch / average launch duration (the
-        # figure rocprofv3's per-kernel average reproduces).
+        # launch duration (HIP events on each launch's own stream, rank 0's
+        # tile; the figure rocprofv3's per-kernel average reproduces).
+        # Wavefront: isect_queue_kernel, 44 B per ray cast.  Fused:
+        # render_fused_kernel, whose only HBM stream is the per-sample film
+        # write (12 B per path; rays stay in registers).  The wavefront runs K
+        # sub-wavefronts on K streams, so isect launches overlap: `chip_busy`
+        # divides the bytes of all launches by the union of their intervals
+        # (the time the isect kernel occupies the chip).  `valu` is the VALU
+        # issue rate over that busy time from the committed PMC pass, against
+        # the chip's wave64 VALU issue peak: traversal is issue- and
+        # latency-bound, not HBM-bound.
         fused = bool(st.get("fused"))
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
@@ -225,12 +229,18 @@ def main():
             total_bytes = agg["ray_casts"] * ISECT_BYTES_PER_CAST
         bytes_per_launch = total_bytes / launches
         busy_ms = agg["isect_busy_ms"]
-        achieved = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+        achieved_busy = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
         per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic, traffic_src = None, None
-        if args.config == 1 and not fused and world == 1 and os.path.exists(TRAFFIC_JSON):  # PMC passes (profiles/)
-            tj = json.load(open(TRAFFIC_JSON))
-            traffic, traffic_src = round(tj["traffic_bytes_per_launch"]), tj["source"][0].rsplit("/", 1)[0]
+        pmc = None
+        if args.config == 1 and not fused and world == 1 and os.path.exists(PMC_JSON):  # PMC passes (profiles/)
+            pmc = json.load(open(PMC_JSON))
+        traffic = round(pmc["traffic_bytes_per_launch"]) if pmc and "traffic_bytes_per_launch" in pmc else None
+        valu = None
+        if pmc and "valu_insts_per_launch" in pmc and busy_ms > 0:
+            rate = pmc["valu_insts_per_launch"] * launches / (busy_ms * 1e-3) / 1e9
+            valu = {"insts_per_launch": round(pmc["valu_insts_per_launch"]), "achieved": round(rate, 1),
+                    "peak": VALU_PEAK_G, "unit": "G wave64 VALU instr/s over isect busy time",
+                    "frac": round(rate / VALU_PEAK_G, 4)}
         rec = {
             "metric": "Mpaths/sec (pixels x spp / s), mitsuba.obj-standin 1024^2 x 64spp, depth 8"
                       if args.config == 1 else f"Mpaths/sec (pixels x spp / s), BASELINE config {args.config}",
@@ -251,16 +261,19 @@ def main():
                                       if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
                        "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "traffic_source": traffic_src,
+            "roofline": {"bound": "hbm", "achieved": round(per_launch, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(per_launch / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",
-                         "launches_per_step": round(launches / args.steps, 2),
-                         "busy_ms_per_step": round(busy_ms / args.steps, 4),
-                         "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                         "per_launch": {"achieved": round(per_launch, 2), "frac": round(per_launch / HBM_PEAK_GBS, 5)},
-                         "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None},
+                         "avg_launch_ms": round(avg_ms, 4),
+                         "launches_per_step": round(launches / args.steps, 2),
+                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None,
+                         "chip_busy": {"busy_ms_per_step": round(busy_ms / args.steps, 4),
+                                       "achieved": round(achieved_busy, 2),
+                                       "frac": round(achieved_busy / HBM_PEAK_GBS, 5),
+                                       "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4)
+                                       if busy_ms else None},
+                         "valu": valu},
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
                                    (("isect_ms", "shade_ms", "camera_ms", "resolve_ms") if args.timing_all
                                     else ("isect_ms",))},

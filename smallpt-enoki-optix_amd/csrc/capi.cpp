@@ -753,6 +753,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         I.next = &b.cnt->isect_next;
         I.refill_idle = env_u32("SPT_REFILL_IDLE", kRefillIdle, 1, 64);
         I.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 160, 0, 255);
+        I.xcd_remap = env_u32("SPT_XCD", 3, 0, 3) & 1u;
         I.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
         // each stream's persistent grid covers 1/K of the chip (measured best)
         I.grid_q8 = env_u32("SPT_ISECT_GRID_Q8", 256u / (uint32_t)K, 0, 4096);
@@ -762,6 +763,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         S.sfilm = sfilm;
         S.stats = ws.stats->stats;
         S.P = (uint32_t)P; S.W = p.width; S.max_depth = p.max_depth;
+        S.xcd_remap = (env_u32("SPT_XCD", 3, 0, 3) >> 1) & 1u;
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
         S.tile_index = p.tile_index; S.tile_count = p.tile_count; S.rows_per_group = p.rows_per_group;
         S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];

@@ -157,13 +157,16 @@ struct Tracer {
 // relative to the exact quantised planes (which already enclose the child),
 // so culling stays conservative and the closest hit is the exact Woop one.
 constexpr float kMarginRel = 1e-6f;
+#ifndef SPT_BRANCHLESS_MASK
+#define SPT_BRANCHLESS_MASK 1
+#endif
 constexpr float kMinDir = 1e-20f;
 
 struct Tracer8 {
     WoopRay wr;
     V3 o;
     float ix, iy, iz, tmin;
-    uint32_t oct_inv;
+    uint32_t oct_rep;  // the ray's inverted octant (0..7) replicated in every byte
     uint32_t nbase, nhits, tbase, thits;
     uint32_t sp;
     bool anyhit, done;
@@ -181,7 +184,8 @@ struct Tracer8 {
         // it, and the triangle test keeps its own correctly rounded divides
         ix = __builtin_amdgcn_rcpf(dx); iy = __builtin_amdgcn_rcpf(dy); iz = __builtin_amdgcn_rcpf(dz);
         const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
-        oct_inv = oct ^ 7u;
+        const uint32_t oct_inv = oct ^ 7u;
+        oct_rep = oct_inv * 0x01010101u;
         tmin = tmin_;
         anyhit = anyhit_;
         nbase = 0;
@@ -214,6 +218,17 @@ struct Tracer8 {
         const uint32_t eyl = py ? w2.z : w4.x, eyh = py ? w2.w : w4.y, xyl = py ? w4.x : w2.z, xyh = py ? w4.y : w2.w;
         const uint32_t ezl = pz ? w3.x : w4.z, ezh = pz ? w3.y : w4.w, xzl = pz ? w4.z : w3.x, xzh = pz ? w4.w : w3.y;
         uint32_t hm = 0;
+#if SPT_BRANCHLESS_MASK
+        // inner children's meta bytes 0b001_11sss (24 + slot) take the ray's
+        // octant in their low 3 bits (byte-wise, once per meta word), so every
+        // child contributes (m >> 5) << (m & 31) with no branch.  A byte is an
+        // inner child iff its bits 3 and 4 are set (leaf offsets are < 24).
+        const auto octx = [&](uint32_t mw) {
+            const uint32_t t8 = mw & (mw >> 1) & 0x08080808u;  // 0x08 in inner bytes
+            return mw ^ ((t8 - (t8 >> 3)) & oct_rep);          // 0x07 & octant
+        };
+        const uint32_t mlo = octx(w1.z), mhi = octx(w1.w);
+#endif
 #pragma unroll
         for (uint32_t c = 0; c < 8; c++) {
             const uint32_t sh = (c & 3u) * 8u;
@@ -226,12 +241,18 @@ struct Tracer8 {
             const float txz = fmaf((float)(((lo ? xzl : xzh) >> sh) & 0xffu), az, bzx);
             const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tmin));
             const float tf = fminf(fminf(txx, txy), fminf(txz, h.t));
+#if SPT_BRANCHLESS_MASK
+            const uint32_t mw = lo ? mlo : mhi;
+            const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);
+            hm = (tn <= tf) ? (hm | bits) : hm;
+#else
             if (tn <= tf) {
                 const uint32_t m = ((lo ? w1.z : w1.w) >> sh) & 0xffu;
                 uint32_t shift = m & 31u;
-                if ((imask >> c) & 1u) shift ^= oct_inv;
+                if ((imask >> c) & 1u) shift ^= oct_rep & 7u;
                 hm |= (m >> 5) << shift;
             }
+#endif
         }
         nbase = w1.x;
         tbase = w1.y;
@@ -271,7 +292,7 @@ struct Tracer8 {
         }
         stats.node();
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
-        const uint32_t slot = (bit - 24u) ^ oct_inv;
+        const uint32_t slot = ((bit - 24u) ^ oct_rep) & 7u;
         const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
         nhits &= ~(1u << bit);
         if (nhits & 0xff000000u) {
@@ -319,7 +340,8 @@ void isect_queue_kernel(IsectQueueArgs a) {
     bool busy = false;
     // wave-uniform pool state
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
-    const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t blk = a.xcd_remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t wave_id = blk * (kIsectBlock / 64) + (threadIdx.x >> 6);
     const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
     const uint32_t dyn_base = share * nwaves;
     uint32_t pool = wave_id * share, pool_end = pool + share;
@@ -472,8 +494,11 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
     __shared__ uint32_t s_stats[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t i = blockIdx.x * kShadeBlock + tid;
     const uint32_t n = *a.count_in;
+    // the grid may be sized from a stale (larger) count: remap only the
+    // blocks that hold queued paths, so every XCD gets its eighth of them
+    const uint32_t nreal = min(gridDim.x, (n + kShadeBlock - 1) / kShadeBlock);
+    const uint32_t i = (a.xcd_remap && blockIdx.x < nreal ? xcd_block(blockIdx.x, nreal) : blockIdx.x) * kShadeBlock + tid;
     if (tid < 2) s_stats[tid] = 0;
 
     // ---- phase 1: survive or terminate (the bounce inputs load alongside)

@@ -56,6 +56,7 @@ struct IsectQueueArgs {
     uint32_t static_share_q8;        // static share of the queue per wave, in 1/256ths
     uint32_t chunk;                  // dynamic chunk (rays per atomic)
     uint32_t grid_q8;                // persistent grid scale in 1/256ths of full occupancy (0 = full)
+    uint32_t xcd_remap;              // 1: blocks sharing an XCD take adjacent static shares
     unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
 };
 
@@ -70,6 +71,16 @@ struct IsectPublicArgs {
     int32_t closest;
 };
 
+// Blocks are dealt round-robin over the 8 XCDs (block b and b + 8 share one
+// L2; MI355X_MICROARCH.md, workgroup dispatch).  This maps the launch's blocks
+// so that those sharing an XCD take adjacent logical indices: each XCD then
+// works on a contiguous eighth of the queue (speed only, never correctness).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t full = nb & ~7u;
+    if (b >= full) return b;
+    return (b & 7u) * (full >> 3) + (b >> 3);
+}
+
 struct ShadeArgs {
     DeviceScene sc;
     PathQueue in, out;
@@ -81,6 +92,7 @@ struct ShadeArgs {
     uint32_t P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     float env_r, env_g, env_b;
+    uint32_t xcd_remap;         // 1: blocks sharing an XCD take adjacent slot ranges
 };
 
 // Starts new paths in queue slots [*surv, capacity): work item w (sample-major:

@@ -39,6 +39,7 @@ for s in "$@"; do
     prof2|prof4) run $s 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$s -o run --output-format csv -- python bench.py --config ${s#prof} --steps 1 --warmup 1 --no-cpu-baseline ;;
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmc) run pmc 900 bash tools/pmc_isect.sh gpurun_out/pmc ;;
     trav) run trav 600 python tools/trav_stats.py ;;
     tilesim) run tilesim 400 python tools/tile_sim.py ;;
     tilesimt) run tilesimt 400 python tools/tile_sim.py --timing ;;
