@@ -11,6 +11,17 @@
 namespace spt {
 
 // ------------------------------------------------------------- traversal
+// woop_test's double-precision fallback re-reads the triangle (rare path) so
+// the single-precision path need not keep the sheared vertices live.
+struct TriReload {
+    const float4* tp;
+    __device__ __forceinline__ void operator()(V3& a, V3& b, V3& c) const {
+        const float* f = (const float*)tp;
+        const auto ld = [f](int i) { return __builtin_nontemporal_load(f + i); };
+        a = v3(ld(0), ld(1), ld(2)); b = v3(ld(4), ld(5), ld(6)); c = v3(ld(8), ld(9), ld(10));
+    }
+};
+
 struct TraceHit {
     int32_t slot;
     uint32_t id;
@@ -130,7 +141,7 @@ struct Tracer {
             const uint32_t s = first + i;
             const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
             float t, u, v;
-            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), tmin, h.t, t, u, v)) {
+            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
                 const uint32_t id = f2u(t0.w);
                 if (t < h.t || id < h.id) {
                     h.t = t;
@@ -157,6 +168,9 @@ struct Tracer {
 // relative to the exact quantised planes (which already enclose the child),
 // so culling stays conservative and the closest hit is the exact Woop one.
 constexpr float kMarginRel = 1e-6f;
+#ifndef SPT_MERGED_STEP
+#define SPT_MERGED_STEP 2
+#endif
 #ifndef SPT_BRANCHLESS_MASK
 #define SPT_BRANCHLESS_MASK 1
 #endif
@@ -168,6 +182,9 @@ struct Tracer8 {
     float ix, iy, iz, tmin;
     uint32_t oct_rep;  // the ray's inverted octant (0..7) replicated in every byte
     uint32_t nbase, nhits, tbase, thits;
+#if SPT_MERGED_STEP >= 2
+    uint32_t tbase2, thits2;  // a second triangle group, queued behind (tbase, thits)
+#endif
     uint32_t sp;
     bool anyhit, done;
     TraceHit h;
@@ -192,6 +209,10 @@ struct Tracer8 {
         nhits = (1u << (24u + oct_inv)) | 1u;  // the root as slot 0 of a virtual parent
         tbase = 0;
         thits = 0;
+#if SPT_MERGED_STEP >= 2
+        tbase2 = 0;
+        thits2 = 0;
+#endif
         sp = 0;
         done = sc.empty != 0;
         h.slot = -1; h.id = 0xffffffffu; h.t = tmax_; h.u = 0.0f; h.v = 0.0f;
@@ -199,7 +220,11 @@ struct Tracer8 {
 
     __device__ __forceinline__ void visit(const DeviceScene& sc, uint32_t node) {
         const uint4* np = sc.nodes8 + (size_t)node * kNode8Quads;
-        const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+        visit_words(np[0], np[1], np[2], np[3], np[4]);
+    }
+
+    __device__ __forceinline__ void visit_words(const uint4 w0, const uint4 w1, const uint4 w2, const uint4 w3,
+                                                const uint4 w4) {
         const uint32_t ew = w0.w;
         const uint32_t imask = ew >> 24;
         const float ax = u2f((ew & 0xffu) << 23) * ix;
@@ -255,11 +280,92 @@ struct Tracer8 {
 #endif
         }
         nbase = w1.x;
-        tbase = w1.y;
         nhits = (hm & 0xff000000u) | imask;
+#if SPT_MERGED_STEP >= 2
+        if (thits) {  // the current group still has triangles: queue the new one
+            tbase2 = w1.y;
+            thits2 = hm & 0x00ffffffu;
+            return;
+        }
+#endif
+        tbase = w1.y;
         thits = hm & 0x00ffffffu;
     }
 
+    __device__ __forceinline__ bool tri_test(const DeviceScene& sc, const float4 t0, const float4 t1, const float4 t2,
+                                             uint32_t s) {
+        float t, u, v;
+        if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
+                      TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
+            const uint32_t id = f2u(t0.w);
+            if (t < h.t || id < h.id) {
+                h.t = t;
+                h.id = id;
+                h.slot = (int32_t)s;
+                h.u = u;
+                h.v = v;
+            }
+            return true;
+        }
+        return false;
+    }
+
+#if SPT_MERGED_STEP
+    // One step = at most one triangle test and one node visit, their loads in
+    // flight together: a lane whose triangle group is down to its last
+    // triangle also visits its next node (the visit may start a new group),
+    // so most triangle tests cost no dependent memory round trip of their own.
+    // The visit culls against the hit the triangle test just made.
+    template <typename Stats>
+    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+        stats.step();
+#if SPT_MERGED_STEP >= 2
+        if (!thits) {
+            tbase = tbase2;
+            thits = thits2;
+            thits2 = 0u;
+        }
+#endif
+        const bool has_tri = thits != 0u;
+        const bool has_node = (nhits & 0xff000000u) != 0u || sp != 0u;
+        if (!has_tri && !has_node) { done = true; return true; }
+#if SPT_MERGED_STEP >= 2
+        const bool do_node = has_node && thits2 == 0u;  // a free slot for the visit's triangles
+#else
+        const bool do_node = has_node && (thits & (thits - 1u)) == 0u;
+#endif
+        // loads are unconditional (idle sides read slot / node 0, always
+        // cached) so both sets are in flight before either is waited on
+        const uint32_t s = has_tri ? tbase + (uint32_t)__builtin_ctz(thits) : 0u;
+        if (has_tri) stats.tri();
+        thits &= thits - 1u;
+        const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
+        if (do_node && !(nhits & 0xff000000u)) {
+            sp--;
+            nbase = stk[(2 * sp) * kIsectBlock];
+            nhits = stk[(2 * sp + 1) * kIsectBlock];
+        }
+        const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits | 1u);
+        const uint32_t slot = ((bit - 24u) ^ oct_rep) & 7u;
+        const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
+        const uint32_t node = do_node ? child : 0u;
+        if (do_node) {
+            stats.node();
+            nhits &= ~(1u << bit);
+            if (nhits & 0xff000000u) {
+                stk[(2 * sp) * kIsectBlock] = nbase;
+                stk[(2 * sp + 1) * kIsectBlock] = nhits;
+                sp++;
+                stats.push(sp);
+            }
+        }
+        const uint4* np = sc.nodes8 + (size_t)node * kNode8Quads;
+        const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+        if (has_tri && tri_test(sc, t0, t1, t2, s) && anyhit) { done = true; return true; }
+        if (do_node) visit_words(w0, w1, w2, w3, w4);
+        return false;
+    }
+#else
     template <typename Stats>
     __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
         stats.step();
@@ -269,7 +375,8 @@ struct Tracer8 {
             thits &= thits - 1u;
             const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
             float t, u, v;
-            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), tmin, h.t, t, u, v)) {
+            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
+                          TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
                 const uint32_t id = f2u(t0.w);
                 if (t < h.t || id < h.id) {
                     h.t = t;
@@ -304,6 +411,7 @@ struct Tracer8 {
         visit(sc, child);
         return false;
     }
+#endif
 };
 
 template <typename Tr, typename Stats = NoStats>

@@ -181,8 +181,11 @@ SPT_HD V3 camera_sample_dir(const Camera& c, uint32_t px, uint32_t py, V3 pos, f
 // p = (1-u-v) v0 + u v1 + v v2.
 struct WoopRay {
     V3 o;
-    int kx, ky, kz;
+    uint32_t k;  // kx | ky << 2 | kz << 4 (one register on the device)
     float Sx, Sy, Sz;
+    SPT_HD int kx() const { return (int)(k & 3u); }
+    SPT_HD int ky() const { return (int)((k >> 2) & 3u); }
+    SPT_HD int kz() const { return (int)(k >> 4); }
 };
 SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
@@ -192,28 +195,61 @@ SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     float dkz = comp(d, kz);
     if (dkz < 0.0f) { int tmp = kx; kx = ky; ky = tmp; }
     WoopRay r;
-    r.o = o; r.kx = kx; r.ky = ky; r.kz = kz;
+    r.o = o; r.k = (uint32_t)kx | (uint32_t)ky << 2 | (uint32_t)kz << 4;
     r.Sx = comp(d, kx) / dkz;
     r.Sy = comp(d, ky) / dkz;
     r.Sz = 1.0f / dkz;
     return r;
 }
 
-// Returns true with t/u/v when hit at t in [tmin, tmax] (NaN-safe).
-SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, float tmin, float tmax,
-                      float& t_out, float& u_out, float& v_out) {
+// The sheared, permuted vertices (Woop et al. 2013 §3).
+struct WoopShear {
+    float Akz, Bkz, Ckz, Ax, Ay, Bx, By, Cx, Cy;
+};
+SPT_HD WoopShear woop_shear(const WoopRay& r, V3 p0, V3 p1, V3 p2) {
     V3 A = p0 - r.o, B = p1 - r.o, C = p2 - r.o;
-    float Akz = comp(A, r.kz), Bkz = comp(B, r.kz), Ckz = comp(C, r.kz);
-    float Ax = comp(A, r.kx) - r.Sx * Akz, Ay = comp(A, r.ky) - r.Sy * Akz;
-    float Bx = comp(B, r.kx) - r.Sx * Bkz, By = comp(B, r.ky) - r.Sy * Bkz;
-    float Cx = comp(C, r.kx) - r.Sx * Ckz, Cy = comp(C, r.ky) - r.Sy * Ckz;
-    float U = Cx * By - Cy * Bx;
-    float V = Ax * Cy - Ay * Cx;
-    float W = Bx * Ay - By * Ax;
+    const int kx = r.kx(), ky = r.ky(), kz = r.kz();
+    WoopShear w;
+    w.Akz = comp(A, kz); w.Bkz = comp(B, kz); w.Ckz = comp(C, kz);
+    w.Ax = comp(A, kx) - r.Sx * w.Akz; w.Ay = comp(A, ky) - r.Sy * w.Akz;
+    w.Bx = comp(B, kx) - r.Sx * w.Bkz; w.By = comp(B, ky) - r.Sy * w.Bkz;
+    w.Cx = comp(C, kx) - r.Sx * w.Ckz; w.Cy = comp(C, ky) - r.Sy * w.Ckz;
+    return w;
+}
+
+struct NoReload {  // the vertices stay in registers (host)
+    V3 p0, p1, p2;
+    SPT_HD void operator()(V3& q0, V3& q1, V3& q2) const { q0 = p0; q1 = p1; q2 = p2; }
+};
+
+// Returns true with t/u/v when hit at t in [tmin, tmax] (NaN-safe).  The
+// double-precision edge fallback (an edge function exactly 0) re-derives the
+// sheared vertices from reload() — on the device a re-read of the triangle,
+// so the single-precision path does not keep them live.
+template <typename Reload>
+SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
+                      float& t_out, float& u_out, float& v_out) {
+    const WoopShear w = woop_shear(r, p0, p1, p2);
+    const float Akz = w.Akz, Bkz = w.Bkz, Ckz = w.Ckz;
+    float U = w.Cx * w.By - w.Cy * w.Bx;
+    float V = w.Ax * w.Cy - w.Ay * w.Cx;
+    float W = w.Bx * w.Ay - w.By * w.Ax;
     if (U == 0.0f || V == 0.0f || W == 0.0f) {
-        U = (float)((double)Cx * (double)By - (double)Cy * (double)Bx);
-        V = (float)((double)Ax * (double)Cy - (double)Ay * (double)Cx);
-        W = (float)((double)Bx * (double)Ay - (double)By * (double)Ax);
+        V3 q0, q1, q2;
+        reload(q0, q1, q2);
+        const WoopShear x = woop_shear(r, q0, q1, q2);
+        // px qy - py qx for (p, q) = (C, B), (A, C), (B, A): one per iteration
+        // of a rolled loop (the rotation keeps few doubles live at a time)
+        float px = x.Cx, py = x.Cy, qx = x.Bx, qy = x.By, rx = x.Ax, ry = x.Ay;
+        float e0 = 0.0f, e1 = 0.0f, e2 = 0.0f;
+#pragma unroll 1
+        for (int i = 0; i < 3; i++) {
+            const float e = (float)((double)px * (double)qy - (double)py * (double)qx);
+            e0 = e1; e1 = e2; e2 = e;
+            const float tx = rx, ty = ry;
+            rx = qx; ry = qy; qx = px; qy = py; px = tx; py = ty;
+        }
+        U = e0; V = e1; W = e2;
     }
     if ((U < 0.0f || V < 0.0f || W < 0.0f) && (U > 0.0f || V > 0.0f || W > 0.0f)) return false;
     float det = (U + V) + W;
