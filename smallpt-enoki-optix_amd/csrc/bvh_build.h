@@ -33,7 +33,8 @@ BvhBuildResult build_bvh(const float* tri_verts, uint64_t ntri, uint32_t max_lea
 // Compressed 8-wide BVH (80 B per node = 20 words, see kernels.hip Tracer8):
 //   w0-2  p.xyz        quantisation origin (f32)
 //   w3    ex | ey<<8 | ez<<16 | imask<<24   (biased exponents; imask: inner slots)
-//   w4    child_base   first inner child (inner children are contiguous, slot order)
+//   w4    child_base   first inner child (inner children are contiguous, slot order);
+//                      on the device (gpu_bvh8_holes) child s sits at w4 + s, w4 % 8 == 0
 //   w5    tri_base     first triangle slot of this node's leaves (contiguous)
 //   w6-7  meta[8]      0 empty; inner 0b001_(24+s); leaf unary(count)<<5 | offset
 //   w8-9  qlo.x[8]  w10-11 qlo.y[8]  w12-13 qlo.z[8]

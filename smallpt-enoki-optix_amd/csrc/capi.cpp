@@ -303,7 +303,19 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     (void)hipGetDevice(&sc->device);
     sc->ntri = ntri;
     sc->stack_depth = bvh8_stack_entries(g.depth);
-    sc->nodes8 = (uint4*)g.nodes8;
+    uint32_t nslots = 0;
+    {
+        uint32_t* holes = nullptr;
+        const hipError_t he = gpu_bvh8_holes(g.nodes8, g.nnodes, s, &holes, &nslots);
+        (void)hipFree(g.nodes8);
+        if (he) {
+            (void)hipFree(g.slot2tri);
+            delete sc;
+            return fail(he == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP, "spt_scene_create (BVH8 layout): %s",
+                        hipGetErrorString(he));
+        }
+        sc->nodes8 = (uint4*)holes;
+    }
     auto bail = [&](hipError_t e) {
         (void)hipFree(g.slot2tri);
         sc->release();
@@ -336,7 +348,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     ss.max_leaf = 3;
     ss.bvh_width = 8;
     ss.builder = SPT_BUILD_GPU_PLOC;
-    ss.device_bytes = (uint64_t)g.nnodes * kNode8Quads * 16 + ntri * 3 * 16 * 2 + (with_tc ? ntri * 24 : 0) + ntri * 4;
+    ss.device_bytes = (uint64_t)nslots * kNode8Quads * 16 + ntri * 3 * 16 * 2 + (with_tc ? ntri * 24 : 0) + ntri * 4;
     ss.build_ms = now_ms() - t0;
     ss.sah_cost = g.sah_cost;
     *out = sc;
@@ -505,13 +517,24 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
     sc->stack_depth = use8 ? bvh8_stack_entries(bvh8.depth) : std::max<uint32_t>(1, bvh.max_depth + 1);
     const float one[3] = {1.0f, 1.0f, 1.0f};
     spt_status us = SPT_OK;
+    uint32_t nslots = 0;
     if (use8) {
-        // pad each 80-B node to its own 128-B cache line (kNode8Quads x 16 B)
+        // pad each 80-B node to its own 128-B cache line (kNode8Quads x 16 B),
+        // then re-lay it on the device with the children at w4 + slot
         const size_t nn = bvh8.nodes.size() / 20;
         std::vector<uint32_t> padded(nn * kNode8Quads * 4, 0u);
         for (size_t i = 0; i < nn; i++)
             std::memcpy(&padded[i * kNode8Quads * 4], &bvh8.nodes[i * 20], 80);
-        if (!us) us = upload(&sc->nodes8, padded.data(), padded.size() * sizeof(uint32_t));
+        uint32_t* compact = nullptr;
+        if (!us) us = upload(&compact, padded.data(), padded.size() * sizeof(uint32_t));
+        if (!us) {
+            uint32_t* holes = nullptr;
+            const hipError_t he = gpu_bvh8_holes(compact, (uint32_t)nn, nullptr, &holes, &nslots);
+            if (he) us = fail(he == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP,
+                              "spt_scene_create (BVH8 layout): %s", hipGetErrorString(he));
+            else sc->nodes8 = (uint4*)holes;
+        }
+        hfree(compact);
     } else {
         if (!us) us = upload(&sc->nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
     }
@@ -533,7 +556,7 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
     ss.max_depth = use8 ? bvh8.depth : bvh.max_depth;
     ss.max_leaf = use8 ? 3 : bvh.max_leaf;
     ss.bvh_width = use8 ? 8 : 2;
-    ss.device_bytes = (use8 ? bvh8.nodes.size() / 20 * kNode8Quads * 16 : bvh.nodes.size() * 4) +
+    ss.device_bytes = (use8 ? (uint64_t)nslots * kNode8Quads * 16 : bvh.nodes.size() * 4) +
                       (h_tris.size() + h_snrm.size()) * 16 +
                       h_tc.size() * 4 + h_o2s.size() * 4;
     ss.build_ms = t1 - t0;
@@ -668,7 +691,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // Traversal counters exist in the wavefront isect kernel only.
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
     const uint32_t fused_env = env_u32("SPT_FUSED", 2, 0, 2);
-    bool fused = fused_env == 2 ? P * p.spp <= 2 * C : fused_env == 1;
+    bool fused = fused_env == 2 ? P * p.spp <= C : fused_env == 1;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
     if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));

@@ -21,6 +21,16 @@ struct GpuBvh8 {
 // out->nodes8 and out->slot2tri (hipFree).  Synchronises stream s.
 hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out);
 
+// Re-lays a compact BVH8 (both builders' output: nnodes nodes of kNode8Quads
+// quads, the inner children of a node contiguous from w4 in slot order) so
+// that every child sits at w4 + slot: 8 slots per node that has inner
+// children, w4 a multiple of 8, the slots of leaf and empty children unused
+// ("holes").  The traversal then finds a child without a popcount and keeps
+// one word per stack entry (hit bits + w4 / 8).  Root stays at slot 0.  On
+// success the caller owns *out (device, *nslots nodes).  Synchronises s.
+hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t nnodes, hipStream_t s, uint32_t** out,
+                          uint32_t* nslots);
+
 }  // namespace spt
 
 namespace spt {

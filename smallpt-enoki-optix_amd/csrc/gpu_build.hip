@@ -536,7 +536,87 @@ struct Temp {
         if (e_ != hipSuccess) return e_;      \
     } while (0)
 
+// Holes layout (gpu_bvh8_holes): flag nodes with inner children; their
+// exclusive scan numbers the child groups (group g -> slots 8 (g + 1) ..).
+__global__ __launch_bounds__(kBlock) void holes_flag_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
+                                                            uint32_t* __restrict__ flags) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) flags[i] = (nodes[(size_t)i * kNode8Quads * 4 + 3] >> 24) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void holes_index_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
+                                                             const uint32_t* __restrict__ group,
+                                                             uint32_t* __restrict__ newidx) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0) newidx[0] = 0u;  // the root keeps slot 0
+    const uint32_t* w = nodes + (size_t)i * kNode8Quads * 4;
+    const uint32_t imask = w[3] >> 24;
+    if (!imask) return;
+    const uint32_t base = 8u * (group[i] + 1u), first = w[4];
+    uint32_t r = 0;
+    for (uint32_t s = 0; s < 8; s++)
+        if ((imask >> s) & 1u) newidx[first + r++] = base + s;  // r-th inner child sits in slot s
+}
+
+__global__ __launch_bounds__(kBlock) void holes_copy_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
+                                                            const uint32_t* __restrict__ group,
+                                                            const uint32_t* __restrict__ newidx,
+                                                            uint32_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint4* src = (const uint4*)(nodes + (size_t)i * kNode8Quads * 4);
+    uint4* dst = (uint4*)(out + (size_t)newidx[i] * kNode8Quads * 4);
+    for (uint32_t q = 0; q < kNode8Quads; q++) dst[q] = src[q];
+    uint4 w1 = src[1];
+    w1.x = (src[0].w >> 24) ? 8u * (group[i] + 1u) : 0u;  // w4: first slot of the child group
+    dst[1] = w1;
+}
+
 }  // namespace
+
+hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, uint32_t** out, uint32_t* nslots) {
+    *out = nullptr;
+    *nslots = 0;
+    Temp tmp;
+    uint32_t *flags, *group, *newidx;
+    GB_TRY(tmp.get(&flags, n));
+    GB_TRY(tmp.get(&group, n));
+    GB_TRY(tmp.get(&newidx, n));
+    uint32_t groups = 0;
+    if (n) {
+        hipLaunchKernelGGL(holes_flag_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, flags);
+        GB_TRY(hipGetLastError());
+        size_t bytes = 0;
+        GB_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, flags, group, (int)n, s));
+        char* ws = nullptr;
+        GB_TRY(tmp.get(&ws, bytes));
+        GB_TRY(hipcub::DeviceScan::ExclusiveSum((void*)ws, bytes, flags, group, (int)n, s));
+        uint32_t last[2] = {0u, 0u};
+        GB_TRY(hipMemcpyAsync(&last[0], group + n - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        GB_TRY(hipMemcpyAsync(&last[1], flags + n - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        GB_TRY(hipStreamSynchronize(s));
+        groups = last[0] + last[1];
+    }
+    if (groups >= (1u << 24)) return hipErrorInvalidValue;  // w4 / 8 must fit the 24-bit stack field
+    const size_t slots = 8 * ((size_t)groups + 1);
+    uint32_t* o = nullptr;
+    GB_TRY(dmalloc(&o, slots * kNode8Quads * 4));
+    hipError_t e = hipMemsetAsync(o, 0, slots * kNode8Quads * 16, s);
+    if (!e && n) {
+        hipLaunchKernelGGL(holes_index_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx);
+        hipLaunchKernelGGL(holes_copy_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx, o);
+        e = hipGetLastError();
+    }
+    if (!e) e = hipStreamSynchronize(s);
+    if (e) {
+        (void)hipFree(o);
+        return e;
+    }
+    *out = o;
+    *nslots = (uint32_t)slots;
+    return hipSuccess;
+}
 
 hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out) {
     *out = GpuBvh8();

@@ -158,37 +158,44 @@ struct Tracer {
 };
 
 // Compressed 8-wide BVH traversal (layout: bvh_build.h; after Ylitie et al.
-// 2017).  A "node group" (nbase, nhits) holds the unvisited inner children of
-// one node: hit bits 24..31 at position 24 + (slot ^ oct_inv), so the highest
-// bit is the child nearest for this ray's octant, and the node's inner-slot
-// mask in bits 0..7 (child index = nbase + popc(imask below slot)).  A
-// "triangle group" (tbase, thits) holds the triangles of the hit leaves.
+// 2017).  A "node group" (nhits) holds the unvisited inner children of one
+// node: hit bits 24..31 at position 24 + (slot ^ oct_inv), so the highest bit
+// is the child nearest for this ray's octant, and the node's child base / 8 in
+// bits 0..23 (device layout with holes: child s at base + s).  A "triangle
+// group" (tbase, thits) holds the triangles of the hit leaves.
 // Child slabs are evaluated as t = q * (2^e / d) + (p - o) / d with one fma;
 // each axis is widened by a margin that bounds the fp32 error of that form
 // relative to the exact quantised planes (which already enclose the child),
 // so culling stays conservative and the closest hit is the exact Woop one.
 constexpr float kMarginRel = 1e-6f;
+// Step modes (template argument of Tracer8T): 0 = one triangle test OR one
+// node visit per step; 1 = the last triangle of a group rides along with the
+// next node visit; 2 = as 1 with a second triangle-group slot, so a node visit
+// rides along with any triangle test while that slot is free.
 #ifndef SPT_MERGED_STEP
 #define SPT_MERGED_STEP 2
 #endif
-#ifndef SPT_BRANCHLESS_MASK
-#define SPT_BRANCHLESS_MASK 1
+#ifndef SPT_FUSED_STEP
+#define SPT_FUSED_STEP 2
 #endif
 constexpr float kMinDir = 1e-20f;
 
-struct Tracer8 {
+template <int kStep>
+struct Tracer8T {
     WoopRay wr;
     V3 o;
     float ix, iy, iz, tmin;
     uint32_t oct_rep;  // the ray's inverted octant (0..7) replicated in every byte
-    uint32_t nbase, nhits, tbase, thits;
-#if SPT_MERGED_STEP >= 2
-    uint32_t tbase2, thits2;  // a second triangle group, queued behind (tbase, thits)
-#endif
+    // node group: unvisited hit children in bits 24..31 (bit 24 + (slot ^
+    // octant)), the group's first node / 8 in bits 0..23 (child s of a node
+    // sits at w4 + s, gpu_bvh8_holes) — one word, also one LDS stack entry
+    uint32_t nhits;
+    uint32_t tbase, thits;
+    uint32_t tbase2, thits2;  // kStep 2: a second triangle group, queued behind (tbase, thits)
     uint32_t sp;
     bool anyhit, done;
     TraceHit h;
-    static constexpr uint32_t kStackWords = 2;
+    static constexpr uint32_t kStackWords = 1;
     __device__ __forceinline__ bool finished() const { return done; }
 
     __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_) {
@@ -205,14 +212,11 @@ struct Tracer8 {
         oct_rep = oct_inv * 0x01010101u;
         tmin = tmin_;
         anyhit = anyhit_;
-        nbase = 0;
-        nhits = (1u << (24u + oct_inv)) | 1u;  // the root as slot 0 of a virtual parent
+        nhits = 1u << (24u + oct_inv);  // the root: slot 0 of a virtual group at node 0
         tbase = 0;
         thits = 0;
-#if SPT_MERGED_STEP >= 2
         tbase2 = 0;
         thits2 = 0;
-#endif
         sp = 0;
         done = sc.empty != 0;
         h.slot = -1; h.id = 0xffffffffu; h.t = tmax_; h.u = 0.0f; h.v = 0.0f;
@@ -226,7 +230,6 @@ struct Tracer8 {
     __device__ __forceinline__ void visit_words(const uint4 w0, const uint4 w1, const uint4 w2, const uint4 w3,
                                                 const uint4 w4) {
         const uint32_t ew = w0.w;
-        const uint32_t imask = ew >> 24;
         const float ax = u2f((ew & 0xffu) << 23) * ix;
         const float ay = u2f(((ew >> 8) & 0xffu) << 23) * iy;
         const float az = u2f(((ew >> 16) & 0xffu) << 23) * iz;
@@ -243,7 +246,6 @@ struct Tracer8 {
         const uint32_t eyl = py ? w2.z : w4.x, eyh = py ? w2.w : w4.y, xyl = py ? w4.x : w2.z, xyh = py ? w4.y : w2.w;
         const uint32_t ezl = pz ? w3.x : w4.z, ezh = pz ? w3.y : w4.w, xzl = pz ? w4.z : w3.x, xzh = pz ? w4.w : w3.y;
         uint32_t hm = 0;
-#if SPT_BRANCHLESS_MASK
         // inner children's meta bytes 0b001_11sss (24 + slot) take the ray's
         // octant in their low 3 bits (byte-wise, once per meta word), so every
         // child contributes (m >> 5) << (m & 31) with no branch.  A byte is an
@@ -253,7 +255,6 @@ struct Tracer8 {
             return mw ^ ((t8 - (t8 >> 3)) & oct_rep);          // 0x07 & octant
         };
         const uint32_t mlo = octx(w1.z), mhi = octx(w1.w);
-#endif
 #pragma unroll
         for (uint32_t c = 0; c < 8; c++) {
             const uint32_t sh = (c & 3u) * 8u;
@@ -266,28 +267,18 @@ struct Tracer8 {
             const float txz = fmaf((float)(((lo ? xzl : xzh) >> sh) & 0xffu), az, bzx);
             const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tmin));
             const float tf = fminf(fminf(txx, txy), fminf(txz, h.t));
-#if SPT_BRANCHLESS_MASK
             const uint32_t mw = lo ? mlo : mhi;
             const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);
             hm = (tn <= tf) ? (hm | bits) : hm;
-#else
-            if (tn <= tf) {
-                const uint32_t m = ((lo ? w1.z : w1.w) >> sh) & 0xffu;
-                uint32_t shift = m & 31u;
-                if ((imask >> c) & 1u) shift ^= oct_rep & 7u;
-                hm |= (m >> 5) << shift;
+        }
+        nhits = (hm & 0xff000000u) | (w1.x >> 3);
+        if constexpr (kStep >= 2) {
+            if (thits) {  // the current group still has triangles: queue the new one
+                tbase2 = w1.y;
+                thits2 = hm & 0x00ffffffu;
+                return;
             }
-#endif
         }
-        nbase = w1.x;
-        nhits = (hm & 0xff000000u) | imask;
-#if SPT_MERGED_STEP >= 2
-        if (thits) {  // the current group still has triangles: queue the new one
-            tbase2 = w1.y;
-            thits2 = hm & 0x00ffffffu;
-            return;
-        }
-#endif
         tbase = w1.y;
         thits = hm & 0x00ffffffu;
     }
@@ -310,52 +301,47 @@ struct Tracer8 {
         return false;
     }
 
-#if SPT_MERGED_STEP
+    template <typename Stats>
+    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+        if constexpr (kStep == 0) return step_single(sc, stk, stats);
+        else return step_merged(sc, stk, stats);
+    }
+
     // One step = at most one triangle test and one node visit, their loads in
     // flight together: a lane whose triangle group is down to its last
     // triangle also visits its next node (the visit may start a new group),
     // so most triangle tests cost no dependent memory round trip of their own.
     // The visit culls against the hit the triangle test just made.
     template <typename Stats>
-    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+    __device__ __forceinline__ bool step_merged(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
         stats.step();
-#if SPT_MERGED_STEP >= 2
-        if (!thits) {
-            tbase = tbase2;
-            thits = thits2;
-            thits2 = 0u;
+        if constexpr (kStep >= 2) {
+            if (!thits) {
+                tbase = tbase2;
+                thits = thits2;
+                thits2 = 0u;
+            }
         }
-#endif
         const bool has_tri = thits != 0u;
         const bool has_node = (nhits & 0xff000000u) != 0u || sp != 0u;
         if (!has_tri && !has_node) { done = true; return true; }
-#if SPT_MERGED_STEP >= 2
-        const bool do_node = has_node && thits2 == 0u;  // a free slot for the visit's triangles
-#else
-        const bool do_node = has_node && (thits & (thits - 1u)) == 0u;
-#endif
+        const bool do_node = kStep >= 2 ? has_node && thits2 == 0u     // a free slot for the visit's triangles
+                                        : has_node && (thits & (thits - 1u)) == 0u;
         // loads are unconditional (idle sides read slot / node 0, always
         // cached) so both sets are in flight before either is waited on
         const uint32_t s = has_tri ? tbase + (uint32_t)__builtin_ctz(thits) : 0u;
         if (has_tri) stats.tri();
         thits &= thits - 1u;
         const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
-        if (do_node && !(nhits & 0xff000000u)) {
-            sp--;
-            nbase = stk[(2 * sp) * kIsectBlock];
-            nhits = stk[(2 * sp + 1) * kIsectBlock];
-        }
+        if (do_node && !(nhits & 0xff000000u)) nhits = stk[--sp * kIsectBlock];
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits | 1u);
-        const uint32_t slot = ((bit - 24u) ^ oct_rep) & 7u;
-        const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
+        const uint32_t child = ((nhits & 0x00ffffffu) << 3) | (((bit - 24u) ^ oct_rep) & 7u);
         const uint32_t node = do_node ? child : 0u;
         if (do_node) {
             stats.node();
             nhits &= ~(1u << bit);
             if (nhits & 0xff000000u) {
-                stk[(2 * sp) * kIsectBlock] = nbase;
-                stk[(2 * sp + 1) * kIsectBlock] = nhits;
-                sp++;
+                stk[sp++ * kIsectBlock] = nhits;
                 stats.push(sp);
             }
         }
@@ -365,9 +351,9 @@ struct Tracer8 {
         if (do_node) visit_words(w0, w1, w2, w3, w4);
         return false;
     }
-#else
+
     template <typename Stats>
-    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+    __device__ __forceinline__ bool step_single(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
         stats.step();
         if (thits) {
             stats.tri();
@@ -393,26 +379,22 @@ struct Tracer8 {
             // current group exhausted: pop the next one (stacked groups always
             // hold inner children) and visit its nearest child in this step
             if (sp == 0) { done = true; return true; }
-            sp--;
-            nbase = stk[(2 * sp) * kIsectBlock];
-            nhits = stk[(2 * sp + 1) * kIsectBlock];
+            nhits = stk[--sp * kIsectBlock];
         }
         stats.node();
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
-        const uint32_t slot = ((bit - 24u) ^ oct_rep) & 7u;
-        const uint32_t child = nbase + (uint32_t)__builtin_popcount(nhits & ((1u << slot) - 1u) & 0xffu);
+        const uint32_t child = ((nhits & 0x00ffffffu) << 3) | (((bit - 24u) ^ oct_rep) & 7u);
         nhits &= ~(1u << bit);
         if (nhits & 0xff000000u) {
-            stk[(2 * sp) * kIsectBlock] = nbase;
-            stk[(2 * sp + 1) * kIsectBlock] = nhits;
-            sp++;
+            stk[sp++ * kIsectBlock] = nhits;
             stats.push(sp);
         }
         visit(sc, child);
         return false;
     }
-#endif
 };
+using Tracer8 = Tracer8T<SPT_MERGED_STEP>;       // isect kernels
+using Tracer8F = Tracer8T<SPT_FUSED_STEP>;       // fused trace+shade kernel
 
 template <typename Tr, typename Stats = NoStats>
 __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
@@ -740,7 +722,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 // registers, so there are no queues, compaction or per-bounce launches.  The
 // per-(sample, pixel) film writes are the same, so the image is bit-identical.
 #ifndef SPT_FUSED_WAVES
-#define SPT_FUSED_WAVES 6
+#define SPT_FUSED_WAVES 4
 #endif
 template <typename Tr, bool kEmit>
 __global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
@@ -999,7 +981,7 @@ hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items
 
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const size_t lds = (size_t)a.sc.stack_depth * (a.sc.nodes8 ? 2u : 1u) * kIsectBlock * sizeof(uint32_t);
+    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);  // one word per entry (both layouts)
     hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
@@ -1041,8 +1023,8 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
 
 hipError_t launch_fused(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out) {
     if (a.sc.nodes8)
-        return a.sc.emission ? launch_fused_t<Tracer8, true>(a, s, lanes_out)
-                             : launch_fused_t<Tracer8, false>(a, s, lanes_out);
+        return a.sc.emission ? launch_fused_t<Tracer8F, true>(a, s, lanes_out)
+                             : launch_fused_t<Tracer8F, false>(a, s, lanes_out);
     return a.sc.emission ? launch_fused_t<Tracer, true>(a, s, lanes_out)
                          : launch_fused_t<Tracer, false>(a, s, lanes_out);
 }

@@ -41,7 +41,7 @@ struct DeviceScene {
     uint32_t nmat;
     const float* emission; // 3 per material or null (no emitters)
     uint32_t nemit;
-    uint32_t stack_depth;  // LDS stack entries per lane (BVH8 entries are 2 words)
+    uint32_t stack_depth;  // LDS stack entries per lane (one word each)
     uint32_t empty;        // no triangles
 };
 
