@@ -22,6 +22,21 @@ struct TriReload {
     }
 };
 
+// The block's dynamic LDS: the traversal stacks, [stack_depth][kIsectBlock]
+// words (lane-interleaved: conflict-free), then per-lane 16-B records.  Only
+// wave-uniform values are kept (SGPRs); a lane derives its slot from its lane
+// id, so no per-lane LDS address has to stay live in a VGPR.
+struct Lds {
+    uint32_t* base;
+    uint32_t wbase;  // this wave's first thread index in the block
+};
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ Lds block_lds(uint32_t* base) {
+    return Lds{base, (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u};
+}
+
 struct TraceHit {
     int32_t slot;
     uint32_t id;
@@ -75,7 +90,10 @@ struct Tracer {
     bool anyhit;
     TraceHit h;
 
-    __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_) {
+    static constexpr uint32_t kExtraLds = 0;  // LDS bytes per block besides the stack
+    __device__ __forceinline__ TraceHit hit(const DeviceScene&, const Lds&) const { return h; }
+    __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_,
+                                         const Lds&) {
         o = o_;
         wr = woop_setup(o_, d);
         ix = 1.0f / d.x; iy = 1.0f / d.y; iz = 1.0f / d.z;
@@ -97,8 +115,9 @@ struct Tracer {
     }
 
     template <typename Stats>
-    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+    __device__ __forceinline__ bool step(const DeviceScene& sc, const Lds& L, Stats& stats) {
         stats.step();
+        uint32_t* stk = L.base + L.wbase + lane_id();
         if (node >= 0) {
             stats.node();
             const float4* np = sc.nodes + (size_t)node * 4;
@@ -180,7 +199,11 @@ constexpr float kMarginRel = 1e-6f;
 #endif
 constexpr float kMinDir = 1e-20f;
 
-template <int kStep>
+// kLds: the per-ray Woop constants (Sx, Sy, Sz, axis indices) and the hit
+// record (slot, id, u, v) live in LDS, one 16-B record each per lane after the
+// stack (ds_read_b128 / ds_write_b128, conflict-free), not in VGPRs; only the
+// hit distance stays in a register (every box test reads it).
+template <int kStep, bool kLds>
 struct Tracer8T {
     WoopRay wr;
     V3 o;
@@ -192,15 +215,44 @@ struct Tracer8T {
     uint32_t nhits;
     uint32_t tbase, thits;
     uint32_t tbase2, thits2;  // kStep 2: a second triangle group, queued behind (tbase, thits)
-    uint32_t sp;
+    uint32_t spa;  // byte offset of this lane's stack top in the block's LDS: tid * 4 + depth * 512
     bool anyhit, done;
     TraceHit h;
     static constexpr uint32_t kStackWords = 1;
+    static constexpr uint32_t kExtraLds = kLds ? 2 * kIsectBlock * 16 : 0;
+    static constexpr uint32_t kRow = kIsectBlock * 4;  // bytes per stack level
     __device__ __forceinline__ bool finished() const { return done; }
 
-    __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_) {
+    __device__ __forceinline__ uint32_t* stack_top(const Lds& L) const { return (uint32_t*)((char*)L.base + spa); }
+    // this lane's records (tid * 16 = (spa % kRow) * 4)
+    __device__ __forceinline__ uint4* wrec(const DeviceScene& sc, const Lds& L) const {
+        return (uint4*)((char*)L.base + sc.stack_depth * kRow + (spa & (kRow - 1u)) * 4u);
+    }
+    __device__ __forceinline__ uint4* hrec(const DeviceScene& sc, const Lds& L) const {
+        return wrec(sc, L) + kIsectBlock;
+    }
+    __device__ __forceinline__ TraceHit hit(const DeviceScene& sc, const Lds& L) const {
+        if constexpr (!kLds) return h;
+        const uint4 r = *hrec(sc, L);
+        TraceHit x;
+        x.slot = (int32_t)r.x; x.id = r.y; x.t = h.t; x.u = u2f(r.z); x.v = u2f(r.w);
+        return x;
+    }
+
+    __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_,
+                                         const Lds& L) {
         o = o_;
         wr = woop_setup(o_, d);
+        spa = (L.wbase + lane_id()) * 4u;
+        if constexpr (kLds) {
+            *wrec(sc, L) = make_uint4(f2u(wr.Sx), f2u(wr.Sy), f2u(wr.Sz), wr.k);
+            // "no hit": slot -1, id ~0 (materialised here: a constant vector
+            // hoisted out of the ray loop would occupy four VGPRs throughout)
+            uint32_t none, zero;
+            asm volatile("v_mov_b32 %0, -1" : "=v"(none));
+            asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+            *hrec(sc, L) = make_uint4(none, none, zero, zero);
+        }
         const float dx = fabsf(d.x) < kMinDir ? copysignf(kMinDir, d.x) : d.x;
         const float dy = fabsf(d.y) < kMinDir ? copysignf(kMinDir, d.y) : d.y;
         const float dz = fabsf(d.z) < kMinDir ? copysignf(kMinDir, d.z) : d.z;
@@ -217,7 +269,6 @@ struct Tracer8T {
         thits = 0;
         tbase2 = 0;
         thits2 = 0;
-        sp = 0;
         done = sc.empty != 0;
         h.slot = -1; h.id = 0xffffffffu; h.t = tmax_; h.u = 0.0f; h.v = 0.0f;
     }
@@ -284,8 +335,24 @@ struct Tracer8T {
     }
 
     __device__ __forceinline__ bool tri_test(const DeviceScene& sc, const float4 t0, const float4 t1, const float4 t2,
-                                             uint32_t s) {
+                                             uint32_t s, const Lds& L, const uint4 wk) {
         float t, u, v;
+        if constexpr (kLds) {
+            WoopRay wl;
+            wl.o = o; wl.Sx = u2f(wk.x); wl.Sy = u2f(wk.y); wl.Sz = u2f(wk.z); wl.k = wk.w;
+            if (woop_test(wl, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
+                          TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
+                // accepted means t <= h.t; a tie goes to the smaller original id
+                const uint32_t id = f2u(t0.w);
+                uint4* hr = hrec(sc, L);
+                if (t < h.t || id < hr->y) {
+                    h.t = t;
+                    *hr = make_uint4((uint32_t)s, id, f2u(u), f2u(v));
+                }
+                return true;
+            }
+            return false;
+        }
         if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
                       TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
             const uint32_t id = f2u(t0.w);
@@ -302,9 +369,9 @@ struct Tracer8T {
     }
 
     template <typename Stats>
-    __device__ __forceinline__ bool step(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
-        if constexpr (kStep == 0) return step_single(sc, stk, stats);
-        else return step_merged(sc, stk, stats);
+    __device__ __forceinline__ bool step(const DeviceScene& sc, const Lds& L, Stats& stats) {
+        if constexpr (kStep == 0) return step_single(sc, L, stats);
+        else return step_merged(sc, L, stats);
     }
 
     // One step = at most one triangle test and one node visit, their loads in
@@ -313,7 +380,7 @@ struct Tracer8T {
     // so most triangle tests cost no dependent memory round trip of their own.
     // The visit culls against the hit the triangle test just made.
     template <typename Stats>
-    __device__ __forceinline__ bool step_merged(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+    __device__ __forceinline__ bool step_merged(const DeviceScene& sc, const Lds& L, Stats& stats) {
         stats.step();
         if constexpr (kStep >= 2) {
             if (!thits) {
@@ -323,7 +390,7 @@ struct Tracer8T {
             }
         }
         const bool has_tri = thits != 0u;
-        const bool has_node = (nhits & 0xff000000u) != 0u || sp != 0u;
+        const bool has_node = (nhits & 0xff000000u) != 0u || spa >= kRow;
         if (!has_tri && !has_node) { done = true; return true; }
         const bool do_node = kStep >= 2 ? has_node && thits2 == 0u     // a free slot for the visit's triangles
                                         : has_node && (thits & (thits - 1u)) == 0u;
@@ -333,7 +400,12 @@ struct Tracer8T {
         if (has_tri) stats.tri();
         thits &= thits - 1u;
         const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
-        if (do_node && !(nhits & 0xff000000u)) nhits = stk[--sp * kIsectBlock];
+        uint4 wk = make_uint4(0u, 0u, 0u, 0u);
+        if constexpr (kLds) wk = *wrec(sc, L);
+        if (do_node && !(nhits & 0xff000000u)) {
+            spa -= kRow;
+            nhits = *stack_top(L);
+        }
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits | 1u);
         const uint32_t child = ((nhits & 0x00ffffffu) << 3) | (((bit - 24u) ^ oct_rep) & 7u);
         const uint32_t node = do_node ? child : 0u;
@@ -341,70 +413,66 @@ struct Tracer8T {
             stats.node();
             nhits &= ~(1u << bit);
             if (nhits & 0xff000000u) {
-                stk[sp++ * kIsectBlock] = nhits;
-                stats.push(sp);
+                *stack_top(L) = nhits;
+                spa += kRow;
+                stats.push(spa / kRow);
             }
         }
         const uint4* np = sc.nodes8 + (size_t)node * kNode8Quads;
         const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
-        if (has_tri && tri_test(sc, t0, t1, t2, s) && anyhit) { done = true; return true; }
+        if (has_tri && tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
         if (do_node) visit_words(w0, w1, w2, w3, w4);
         return false;
     }
 
     template <typename Stats>
-    __device__ __forceinline__ bool step_single(const DeviceScene& sc, uint32_t* __restrict__ stk, Stats& stats) {
+    __device__ __forceinline__ bool step_single(const DeviceScene& sc, const Lds& L, Stats& stats) {
         stats.step();
         if (thits) {
             stats.tri();
             const uint32_t s = tbase + (uint32_t)__builtin_ctz(thits);
             thits &= thits - 1u;
             const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
-            float t, u, v;
-            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                          TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
-                const uint32_t id = f2u(t0.w);
-                if (t < h.t || id < h.id) {
-                    h.t = t;
-                    h.id = id;
-                    h.slot = (int32_t)s;
-                    h.u = u;
-                    h.v = v;
-                }
-                if (anyhit) { done = true; return true; }
-            }
+            uint4 wk = make_uint4(0u, 0u, 0u, 0u);
+            if constexpr (kLds) wk = *wrec(sc, L);
+            if (tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
             return false;
         }
         if (!(nhits & 0xff000000u)) {
             // current group exhausted: pop the next one (stacked groups always
             // hold inner children) and visit its nearest child in this step
-            if (sp == 0) { done = true; return true; }
-            nhits = stk[--sp * kIsectBlock];
+            if (spa < kRow) { done = true; return true; }
+            spa -= kRow;
+            nhits = *stack_top(L);
         }
         stats.node();
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
         const uint32_t child = ((nhits & 0x00ffffffu) << 3) | (((bit - 24u) ^ oct_rep) & 7u);
         nhits &= ~(1u << bit);
         if (nhits & 0xff000000u) {
-            stk[sp++ * kIsectBlock] = nhits;
-            stats.push(sp);
+            *stack_top(L) = nhits;
+            spa += kRow;
+            stats.push(spa / kRow);
         }
         visit(sc, child);
         return false;
     }
 };
-using Tracer8 = Tracer8T<SPT_MERGED_STEP>;       // isect kernels
-using Tracer8F = Tracer8T<SPT_FUSED_STEP>;       // fused trace+shade kernel
+#ifndef SPT_LDS_RAY
+#define SPT_LDS_RAY 1
+#endif
+using Tracer8 = Tracer8T<SPT_MERGED_STEP, SPT_LDS_RAY>;  // isect kernels
+using Tracer8F = Tracer8T<SPT_FUSED_STEP, false>;        // fused trace+shade kernel
 
 template <typename Tr, typename Stats = NoStats>
 __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
-                                          bool anyhit, uint32_t* __restrict__ stk, Stats& stats) {
+                                          bool anyhit, const Lds& L, Stats& stats) {
     Tr tr;
-    tr.init(sc, o, d, tmin, tmax, anyhit);
+    tr.init(sc, o, d, tmin, tmax, anyhit, L);
     if (!tr.finished())
-        while (!tr.step(sc, stk, stats)) {
+        while (!tr.step(sc, L, stats)) {
         }
-    return tr.h;
+    return tr.hit(sc, L);
 }
 
 // Persistent wavefront isect over the path queue.  The grid holds only as
@@ -422,7 +490,7 @@ template <typename Tr, bool kStats>
 __global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_ISECT_WAVES, 8)))
 void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
-    uint32_t* stk = lds_stack + threadIdx.x;
+    const Lds L = block_lds(lds_stack);
     const uint32_t n = *a.count;
     typename std::conditional<kStats, TravStats, NoStats>::type st;
     Tr tr;
@@ -459,11 +527,11 @@ void isect_queue_kernel(IsectQueueArgs a) {
                     const V3 d = v3(a.q.dx[ray], a.q.dy[ray], a.q.dz[ray]);
                     const uint32_t depth = a.q.meta[ray] & ((1u << kMetaDepthBits) - 1u);
                     // any-hit for the last cast unless emitters need the surface
-                    tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !a.sc.emission);
-                    busy = true;
-                    if (tr.finished()) {  // empty scene
-                        a.hits[ray] = make_float4(u2f(0xffffffffu), 0.0f, 0.0f, 0.0f);
-                        busy = false;
+                    tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !a.sc.emission, L);
+                    busy = !tr.finished();
+                    if (!busy) {  // empty scene: the miss record init made
+                        const TraceHit hh = tr.hit(a.sc, L);
+                        a.hits[ray] = make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v);
                     }
                 }
                 pool += take;
@@ -472,8 +540,9 @@ void isect_queue_kernel(IsectQueueArgs a) {
         }
         if (!__ballot(busy)) break;
         wave_steps++;
-        if (busy && tr.step(a.sc, stk, st)) {
-            a.hits[ray] = make_float4(u2f((uint32_t)tr.h.slot), tr.h.t, tr.h.u, tr.h.v);
+        if (busy && tr.step(a.sc, L, st)) {
+            const TraceHit hh = tr.hit(a.sc, L);
+            a.hits[ray] = make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v);
             busy = false;
         }
     }
@@ -498,8 +567,8 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
     NoStats st;
     const TraceHit h = a.sc.nodes8
-                           ? trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x, st)
-                           : trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, lds_stack + threadIdx.x, st);
+                           ? trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
+                           : trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
     if (h.slot < 0) {
         a.tri_id[i] = -1;
         return;
@@ -728,7 +797,7 @@ template <typename Tr, bool kEmit>
 __global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     extern __shared__ uint32_t lds_stack[];
-    uint32_t* stk = lds_stack + threadIdx.x;
+    const Lds L = block_lds(lds_stack);
     const uint32_t n = a.count;
     NoStats st;
     Tr tr;
@@ -752,7 +821,8 @@ void render_fused_kernel(FusedArgs a) {
                 pending = false;
                 casts++;
                 bool term = true;
-                const int32_t slot = tr.h.slot;
+                const TraceHit hh = tr.hit(a.sc, L);
+                const int32_t slot = hh.slot;
                 if (slot < 0) {
                     lr = lr + thr * a.env_r;                       // main.cpp:407
                     lg = lg + thg * a.env_g;
@@ -789,7 +859,7 @@ void render_fused_kernel(FusedArgs a) {
                             rng.inc = ((uint64_t)gpix << 1u) | 1u;
                             float xi_x, xi_y;
                             draw2(rng, a.rng_order, xi_x, xi_y);   // main.cpp:413
-                            const float t = tr.h.t, u = tr.h.u, v = tr.h.v;
+                            const float t = hh.t, u = hh.u, v = hh.v;
                             const float w = (1.0f - u) - v;          // add_math.h:6
                             const V3 sn = v3((w * m0.x + u * m1.x) + v * m2.x,  // optix_backend.h:483-484
                                              (w * m0.y + u * m1.y) + v * m2.y,
@@ -800,7 +870,7 @@ void render_fused_kernel(FusedArgs a) {
                             dir = to_world(fr, cosine_hemisphere(xi_x, xi_y));  // main.cpp:418-419, 424
                             rs = rng.state;
                             depth++;
-                            tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit);
+                            tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit, L);
                             busy = true;
                             conts++;
                         }
@@ -843,7 +913,7 @@ void render_fused_kernel(FusedArgs a) {
                     depth = 0;
                     thr = thg = thb = 1.0f;                        // main.cpp:391
                     lr = lg = lb = 0.0f;
-                    tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit);
+                    tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit, L);
                     starts++;
                     busy = true;
                     if (tr.finished()) {  // empty scene: a miss
@@ -856,7 +926,7 @@ void render_fused_kernel(FusedArgs a) {
             }
         }
         if (!__ballot(busy || pending)) break;
-        if (busy && tr.step(a.sc, stk, st)) {
+        if (busy && tr.step(a.sc, L, st)) {
             busy = false;
             pending = true;
         }
@@ -961,7 +1031,7 @@ static uint32_t persistent_blocks(size_t lds) {
 template <typename Tr, bool kStats>
 static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
-    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t);
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
     const uint32_t full = persistent_blocks<Tr, kStats>(lds);
     const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)full * a.grid_q8) >> 8)) : full;
     const uint32_t blocks = min(scaled, blocks_for(grid_items, kIsectBlock));
@@ -981,7 +1051,8 @@ hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items
 
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t);  // one word per entry (both layouts)
+    // one word per stack entry (both layouts), plus the BVH8 tracer's records
+    const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t) + Tracer8::kExtraLds;
     hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
@@ -1000,7 +1071,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
     static thread_local int cached_dev = -1;
-    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t);
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (!cached || cached_lds != lds || cached_dev != dev) {
