@@ -130,9 +130,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # One process per GPU.  SPT_REHEARSE_SHARED_GPU=1 (with SPT_DIST_BACKEND=gloo)
+    # lets N ranks share the GPUs there are, to rehearse the N-rank flow on a
+    # one-GPU box; the default is strict one-rank-per-device over RCCL.
+    if os.environ.get("SPT_REHEARSE_SHARED_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     # scene: generated stand-in, loaded through the OBJ reader like main.cpp:365
     # (rank 0 writes the cached OBJ first)
@@ -196,10 +205,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([agg["ray_casts"], agg["isect_ms"], agg["iterations"]], dtype=torch.float64, device=dev)
+        tot = torch.tensor([agg["ray_casts"], agg["isect_ms"], agg["iterations"]], dtype=torch.float64, device=rdev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         agg_casts_all = float(tot[0].item())
     else:

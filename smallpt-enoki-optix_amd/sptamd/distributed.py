@@ -47,7 +47,16 @@ class TileGather:
         if self.world == 1:
             self.image.copy_(self.tile_view())
             return self.image
-        dist.gather(self.tile, self.gather_list if self.rank == 0 else None, dst=0)
+        if self.tile.is_cuda and dist.get_backend() != "nccl":
+            # gloo gathers host tensors only (the CPU rehearsal of the N-rank flow)
+            tile = self.tile.cpu()
+            glist = [torch.empty_like(tile) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(tile, glist, dst=0)
+            if self.rank == 0:
+                for r in range(self.world):
+                    self.gather_list[r].copy_(glist[r])
+        else:
+            dist.gather(self.tile, self.gather_list if self.rank == 0 else None, dst=0)
         if self.rank != 0:
             return None
         for r in range(self.world):
