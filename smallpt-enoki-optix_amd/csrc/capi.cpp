@@ -61,21 +61,20 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// 64 B per path: rng u64 | 6 ray f32 | pix u32 | meta u32 | 3 throughput f32 | 3 radiance f32
-constexpr size_t kPathBytes = 8 + 6 * 4 + 4 + 4 + 3 * 4 + 3 * 4;
+// 68 B per path: q0, q1, q2 (16 B each), rng_hi (4 B), rad (16 B, emitters)
+constexpr size_t kPathBytes = 3 * 16 + 4 + 16;
 constexpr size_t kHitBytes = 16;
 
-// Planes are `stride` elements apart (stride = cap + pad, see queue_stride).
+// Planes are `stride` elements apart (stride = cap + pad, see queue_stride);
+// the quad planes first, so each stays 16-B aligned.
 PathQueue carve_queue(char* base, size_t stride) {
     PathQueue q;
-    q.rng = (uint64_t*)base;
-    float* f = (float*)(base + 8 * stride);
-    q.ox = f; q.oy = f + stride; q.oz = f + 2 * stride;
-    q.dx = f + 3 * stride; q.dy = f + 4 * stride; q.dz = f + 5 * stride;
-    q.pix = (uint32_t*)(f + 6 * stride);
-    q.meta = q.pix + stride;
-    q.tr = (float*)(q.meta + stride); q.tg = q.tr + stride; q.tb = q.tg + stride;
-    q.lr = q.tb + stride; q.lg = q.lr + stride; q.lb = q.lg + stride;
+    float4* f4 = (float4*)base;
+    q.q0 = f4;
+    q.q1 = f4 + stride;
+    q.q2 = f4 + 2 * stride;
+    q.rad = f4 + 3 * stride;
+    q.rng_hi = (uint32_t*)(f4 + 4 * stride);
     return q;
 }
 

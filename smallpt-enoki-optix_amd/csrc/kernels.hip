@@ -523,9 +523,10 @@ void isect_queue_kernel(IsectQueueArgs a) {
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
                 if (!busy && rank < take) {
                     ray = pool + rank;
-                    const V3 o = v3(a.q.ox[ray], a.q.oy[ray], a.q.oz[ray]);
-                    const V3 d = v3(a.q.dx[ray], a.q.dy[ray], a.q.dz[ray]);
-                    const uint32_t depth = a.q.meta[ray] & ((1u << kMetaDepthBits) - 1u);
+                    const float4 q1 = a.q.q1[ray], q2 = a.q.q2[ray];
+                    const V3 o = v3(q1.x, q1.y, q1.z);
+                    const V3 d = v3(q2.x, q2.y, q2.z);
+                    const uint32_t depth = f2u(q1.w) & ((1u << kMetaDepthBits) - 1u);
                     // any-hit for the last cast unless emitters need the surface
                     tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !a.sc.emission, L);
                     busy = !tr.finished();
@@ -592,15 +593,11 @@ __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32
 __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix,
                                            uint32_t meta, uint64_t rng, float tr, float tg, float tb, float lr,
                                            float lg, float lb, bool with_l) {
-    q.ox[j] = o.x; q.oy[j] = o.y; q.oz[j] = o.z;
-    q.dx[j] = d.x; q.dy[j] = d.y; q.dz[j] = d.z;
-    q.pix[j] = pix;
-    q.meta[j] = meta;
-    q.rng[j] = rng;
-    q.tr[j] = tr; q.tg[j] = tg; q.tb[j] = tb;
-    if (with_l) {  // gathered radiance planes: only scenes with emitters use them
-        q.lr[j] = lr; q.lg[j] = lg; q.lb[j] = lb;
-    }
+    q.q0[j] = make_float4(tr, tg, tb, u2f(pix));
+    q.q1[j] = make_float4(o.x, o.y, o.z, u2f(meta));
+    q.q2[j] = make_float4(d.x, d.y, d.z, u2f((uint32_t)rng));
+    q.rng_hi[j] = (uint32_t)(rng >> 32);
+    if (with_l) q.rad[j] = make_float4(lr, lg, lb, 0.0f);  // only scenes with emitters
 }
 
 // Refill: start work items [cursor, cursor + total) in queue slots
@@ -668,14 +665,15 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
     uint64_t rs = 0;
     if (i < n) {
-        pix = a.in.pix[i];
-        meta = a.in.meta[i];
+        const float4 q0 = a.in.q0[i], q1 = a.in.q1[i];
+        pix = f2u(q0.w);
+        meta = f2u(q1.w);
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
         hit = a.hits[i];
         const int32_t slot = (int32_t)f2u(hit.x);
-        tr = a.in.tr[i]; tg = a.in.tg[i]; tb = a.in.tb[i];
-        if (kEmit) { lr = a.in.lr[i]; lg = a.in.lg[i]; lb = a.in.lb[i]; }
+        tr = q0.x; tg = q0.y; tb = q0.z;
+        if (kEmit) { const float4 l = a.in.rad[i]; lr = l.x; lg = l.y; lb = l.z; }
         bool term = true;
         if (slot < 0) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
@@ -688,9 +686,10 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             if (bounce) {
                 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
                 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
-                rs = a.in.rng[i];
-                o = v3(a.in.ox[i], a.in.oy[i], a.in.oz[i]);
-                d = v3(a.in.dx[i], a.in.dy[i], a.in.dz[i]);
+                const float4 q2 = a.in.q2[i];
+                rs = ((uint64_t)a.in.rng_hi[i] << 32) | f2u(q2.w);
+                o = v3(q1.x, q1.y, q1.z);
+                d = v3(q2.x, q2.y, q2.z);
             }
             uint32_t mat = f2u(m0.w);
             if (kEmit && mat < a.sc.nemit) {

@@ -19,14 +19,18 @@ constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
 constexpr uint32_t kIsectChunk = 128;       // dynamic-share queue indices a wave takes per atomic
 constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
 
-// Path queue, structure of arrays (ray.h layout for the ray planes).
+// Path queue: planes of 16-B quads grouped by who reads them, so a kernel
+// moves a path in a few dwordx4 accesses (one coalesced 1-KB wave instruction
+// each) instead of one 4-B plane per field:
+//   q0 = (tr, tg, tb, pix)        throughput, tile-local pixel  [shade: every path]
+//   q1 = (o.x, o.y, o.z, meta)    origin, sample << 8 | cast    [isect; shade: every path]
+//   q2 = (d.x, d.y, d.z, rng.lo)  direction, PCG32 state lo     [isect; shade: bounces]
+//   rng_hi                        PCG32 state hi (inc = 2 * global_pixel + 1)
+//   rad = (lr, lg, lb, -)         radiance gathered so far (emitters only)
 struct PathQueue {
-    float *ox, *oy, *oz, *dx, *dy, *dz;
-    uint32_t* pix;    // tile-local pixel index
-    uint32_t* meta;   // sample << 8 | cast index
-    uint64_t* rng;    // PCG32 state (inc = 2 * global_pixel + 1)
-    float *tr, *tg, *tb;  // path throughput
-    float *lr, *lg, *lb;  // radiance gathered so far (emission hits)
+    float4 *q0, *q1, *q2;
+    uint32_t* rng_hi;
+    float4* rad;
 };
 
 // Geometry on device, leaf ("slot") order.

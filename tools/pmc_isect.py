@@ -30,10 +30,15 @@ def passes(paths, kernel="isect_queue"):
     return per
 
 
-def main(out, *paths):
-    per = passes(paths)
+def main(out, *args):
+    # trailing argument without ".csv": the kernel-name substring (default isect_queue)
+    kernel = "isect_queue"
+    paths = list(args)
+    if paths and not paths[-1].endswith(".csv"):
+        kernel = paths.pop()
+    per = passes(paths, kernel)
     mean = {c: sum(v.values()) / max(len(v), 1) for c, v in per.items()}
-    rec = {"kernel": "isect_queue_kernel",
+    rec = {"kernel": kernel,
            "dispatches": {c: len(v) for c, v in per.items()},
            "per_launch": mean,
            "source": list(paths)}

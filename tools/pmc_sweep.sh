@@ -13,11 +13,11 @@ i=0
 csvs=""
 for ctrs in "$@"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex isect_queue -d "$out/p$i" -o run --output-format csv \
+  timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex ${KERNEL:-isect_queue} -d "$out/p$i" -o run --output-format csv \
       -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$out/p$i.log" 2>&1
   rc=$?
   echo "== pass $i ($ctrs) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$i.log"; exit $rc; fi
   csvs="$csvs $out/p$i/run_counter_collection.csv"
 done
-python tools/pmc_isect.py "$out/summary.json" $csvs
+python tools/pmc_isect.py "$out/summary.json" $csvs ${KERNEL:-isect_queue}
