@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rows-per-group", type=int, default=8)
     ap.add_argument("--pipeline", default=None, help="wavefront | fused (default: the library's auto choice)")
     ap.add_argument("--timing", action="store_true", help="HIP events around every launch (as bench.py)")
+    ap.add_argument("--wavefront", type=int, default=0, help="paths in flight (0 = the library default)")
     args = ap.parse_args()
     import torch
 
@@ -48,7 +49,8 @@ def main():
     W, H, spp, D = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
     for n in args.tiles:
         p = sptamd.make_params(W, H, spp, D, tile_index=0, tile_count=n, rows_per_group=args.rows_per_group,
-                               timing=args.timing, pipeline=args.pipeline, **kw)
+                               timing=args.timing, pipeline=args.pipeline,
+                               wavefront_paths=args.wavefront, **kw)
         rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
         film = torch.empty((3, rows, W), dtype=torch.float32, device="cuda")
         scene.render(p, film=film)
