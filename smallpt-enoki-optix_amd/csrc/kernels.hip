@@ -462,7 +462,10 @@ struct Tracer8T {
 #define SPT_LDS_RAY 1
 #endif
 using Tracer8 = Tracer8T<SPT_MERGED_STEP, SPT_LDS_RAY>;  // isect kernels
-using Tracer8F = Tracer8T<SPT_FUSED_STEP, false>;        // fused trace+shade kernel
+#ifndef SPT_FUSED_LDS
+#define SPT_FUSED_LDS 1
+#endif
+using Tracer8F = Tracer8T<SPT_FUSED_STEP, SPT_FUSED_LDS>;  // fused trace+shade kernel
 
 template <typename Tr, typename Stats = NoStats>
 __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
@@ -790,7 +793,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 // registers, so there are no queues, compaction or per-bounce launches.  The
 // per-(sample, pixel) film writes are the same, so the image is bit-identical.
 #ifndef SPT_FUSED_WAVES
-#define SPT_FUSED_WAVES 4
+#define SPT_FUSED_WAVES 5
 #endif
 template <typename Tr, bool kEmit>
 __global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
