@@ -88,6 +88,36 @@ def workload(args, scenes):
     return src, kw, True, True
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
+    """Measured HBM peak for the roofline (BASELINE.md plan): a device-to-device
+    copy of nbytes, read + write bytes over the best of reps (HIP events)."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return 2.0 * nbytes / (best * 1e-3) / 1e9
+
+
 def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     """Oracle (oracle/, a C restatement of main.cpp:354-446) on a bounded row
     sample of the same workload, on this host's cores."""
@@ -110,6 +140,7 @@ def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     dt = time.perf_counter() - t0
     paths = rows.size * args.width * args.spp
     return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"{rows.size} of {args.height} rows (evenly spaced) x {args.width} px x {args.spp} spp, "
                       f"depth {args.depth}: {paths} paths, {casts} casts in {dt:.2f} s "
                       f"(oracle: C restatement, median-split BVH, {threads} threads)"}
@@ -209,11 +240,14 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([agg["ray_casts"], agg["isect_ms"], agg["iterations"]], dtype=torch.float64, device=rdev)
+        tot = torch.tensor([agg["ray_casts"], agg["isect_ms"], agg["iterations"], agg["continuations"]],
+                           dtype=torch.float64, device=rdev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         agg_casts_all = float(tot[0].item())
+        agg_cont_all = float(tot[3].item())
     else:
         agg_casts_all = float(agg["ray_casts"])
+        agg_cont_all = float(agg["continuations"])
 
     paths = W * H * args.spp * args.steps
     value = paths / elapsed / 1e6
@@ -241,6 +275,14 @@ def main():
         busy_ms = agg["isect_busy_ms"]
         achieved_busy = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
         per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        # whole-path bytes: B_path = 84 + 120 S + 60 C, S = casts and
+        # C = continuations per path, over the whole frame time, against the spec
+        # peak and a stream-copy peak measured here (BASELINE.md plan)
+        s_bar = agg_casts_all / paths
+        c_bar = agg_cont_all / paths
+        b_path = 84.0 + 120.0 * s_bar + 60.0 * c_bar
+        path_gbs = b_path * paths / elapsed / 1e9
+        copy_gbs = stream_copy_gbs(torch, dev)
         pmc = None
         if args.config == 1 and not fused and world == 1 and os.path.exists(PMC_JSON):  # PMC passes (profiles/)
             pmc = json.load(open(PMC_JSON))
@@ -283,7 +325,12 @@ def main():
                                        "frac": round(achieved_busy / HBM_PEAK_GBS, 5),
                                        "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4)
                                        if busy_ms else None},
-                         "valu": valu},
+                         "valu": valu,
+                         "stream_copy_peak": round(copy_gbs, 1),
+                         "path": {"bytes_per_path": round(b_path, 1),
+                                  "formula": "84 + 120*S + 60*C (SURVEY 8d), S=%.4f C=%.4f" % (s_bar, c_bar),
+                                  "achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
+                                  "frac_of_stream_copy": round(path_gbs / copy_gbs, 4)}},
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
                                    (("isect_ms", "shade_ms", "camera_ms", "resolve_ms") if args.timing_all
                                     else ("isect_ms",))},
