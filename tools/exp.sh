@@ -6,4 +6,4 @@ while read -r name envs; do
   [ -z "$name" ] && continue
   echo "== $name $envs" >> gpurun_out/exp.log
   env $envs timeout -k 10 200 python tools/tile_sim.py --timing ${TS_ARGS:-} 2>&1 | grep -v amdgpu.ids >> gpurun_out/exp.log || exit 1
-done < "${EXP_LIST:-tools/exp_list.txt}"
+done < "${EXP_LIST:?set EXP_LIST to a file of lines: name ENV=val ...}"
