@@ -623,6 +623,7 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
     a.n = n;
     a.closest = do_closest;
+    a.refill_idle = env_u32("SPT_PUBLIC_REFILL_IDLE", kRefillIdle, 1, 64);
     HIP_TRY(launch_isect_public(a, (hipStream_t)stream));
     return SPT_OK;
 }

@@ -583,6 +583,64 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     a.v[i] = h.v;
 }
 
+// The same semantics over the compressed BVH8 as a persistent kernel: a grid
+// of at most the chip's occupancy, each wave owning a contiguous share of the
+// rays (no atomics, so concurrent calls on different streams need no shared
+// counter) and refilling its finished lanes from that share, so lanes do not
+// idle behind a wave's slowest ray.  Masked-off rays take a slot and write
+// nothing (wavefront_isect.cu:86).
+__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_ISECT_WAVES, 8)))
+void isect_public_persistent_kernel(IsectPublicArgs a) {
+    extern __shared__ uint32_t lds_stack[];
+    const Lds L = block_lds(lds_stack);
+    NoStats st;
+    Tracer8 tr;
+    uint32_t ray = 0;
+    bool busy = false;
+    const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
+    const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t share = (uint32_t)(((uint64_t)a.n + nwaves - 1) / nwaves);
+    uint32_t pool = min(a.n, wave_id * share);
+    const uint32_t pool_end = min(a.n, pool + share);
+    while (true) {
+        uint64_t idle = __ballot(!busy);
+        if ((uint32_t)__popcll(idle) >= a.refill_idle) {
+            while (idle && pool < pool_end) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
+                if (!busy && rank < take) {
+                    ray = pool + rank;
+                    const bool m = !a.mask || ((a.mask_size == 1) ? (a.mask[0] != 0) : (a.mask[ray] != 0));
+                    if (m) {
+                        const V3 o = v3(a.ox[ray], a.oy[ray], a.oz[ray]);
+                        const V3 d = v3(a.dx[ray], a.dy[ray], a.dz[ray]);
+                        const float tmin = a.tmin ? a.tmin[ray] : kRayTmin, tmax = a.tmax ? a.tmax[ray] : kRayTmax;
+                        tr.init(a.sc, o, d, tmin, tmax, a.closest == 0, L);
+                        busy = !tr.finished();
+                        if (!busy) a.tri_id[ray] = -1;  // empty scene
+                    }
+                }
+                pool += take;
+                idle = __ballot(!busy);
+            }
+        }
+        if (!__ballot(busy)) break;
+        if (busy && tr.step(a.sc, L, st)) {
+            const TraceHit h = tr.hit(a.sc, L);
+            if (h.slot < 0) {
+                a.tri_id[ray] = -1;
+            } else {
+                a.tri_id[ray] = (int32_t)h.id;
+                a.t[ray] = h.t;
+                a.u[ray] = h.u;
+                a.v[ray] = h.v;
+            }
+            busy = false;
+        }
+    }
+}
+
 // ------------------------------------------------------------ camera gen
 __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32_t order, uint32_t x,
                                            uint32_t y, V3& o, V3& d) {
@@ -1055,6 +1113,33 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     // one word per stack entry (both layouts), plus the BVH8 tracer's records
     const size_t lds = (size_t)a.sc.stack_depth * kIsectBlock * sizeof(uint32_t) + Tracer8::kExtraLds;
+    // one lane per ray by default: the reference's first bounce (camera rays)
+    // traces 25-30 % faster in lockstep waves; the persistent kernel wins on
+    // incoherent rays (+25-36 %) — tools/isect_api_bench.py, DESIGN.md §4
+    const char* pe = getenv("SPT_PUBLIC_PERSISTENT");  // read per call (tests switch it)
+    const bool persistent = pe && atoi(pe) != 0;
+    if (a.sc.nodes8 && persistent) {
+        static thread_local size_t cached_lds = 0;
+        static thread_local uint32_t cached = 0;
+        static thread_local int cached_dev = -1;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (!cached || cached_lds != lds || cached_dev != dev) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_public_persistent_kernel, kIsectBlock,
+                                                             lds) != hipSuccess || per_cu <= 0)
+                per_cu = 1;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+                cus = 256;
+            cached = (uint32_t)(per_cu * cus);
+            cached_lds = lds;
+            cached_dev = dev;
+        }
+        // at least 64 rays per wave (a wave's share), at most the chip's occupancy
+        const uint32_t blocks = max(1u, min(cached, blocks_for(a.n, kIsectBlock / 64 * 64 * 2)));
+        hipLaunchKernelGGL(isect_public_persistent_kernel, dim3(blocks), dim3(kIsectBlock), lds, s, a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }

@@ -73,6 +73,7 @@ struct IsectPublicArgs {
     float *t, *u, *v;
     uint32_t n;
     int32_t closest;
+    uint32_t refill_idle;  // persistent BVH8 kernel: refill a wave once this many lanes are idle
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (block b and b + 8 share one

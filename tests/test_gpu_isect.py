@@ -219,3 +219,38 @@ def test_axis_aligned_and_degenerate_rays(backend, oracle_bvh):
     assert_hits_equal(got, ref)
     assert (got[0][3::6] == -1).all() and (got[0][5::6] == -1).all()
     assert (got[0] >= 0).sum() > n // 10
+
+
+@pytest.mark.parametrize("refill", ["1", "8", "64"])
+def test_persistent_public_kernel(backend, oracle_bvh, monkeypatch, refill):
+    """SPT_PUBLIC_PERSISTENT=1 swaps spt_intersect onto the lane-refill kernel;
+    results must stay bit-identical to the oracle (closest, any-hit occlusion,
+    interval bounds, per-ray and broadcast masks, a ragged ray count)."""
+    monkeypatch.setenv("SPT_PUBLIC_PERSISTENT", "1")
+    monkeypatch.setenv("SPT_PUBLIC_REFILL_IDLE", refill)
+    o, d = random_rays(150_001, 11)
+    ref = oracle_bvh.intersect(o, d)
+    assert_hits_equal(gpu_isect(backend, o, d), ref)
+    anyh = gpu_isect(backend, o, d, closest=False)
+    np.testing.assert_array_equal(anyh[0] >= 0, ref[0] >= 0)
+    rng = np.random.default_rng(12)
+    n = o.shape[1]
+    tmin = rng.uniform(0.0, 1.0, size=n).astype(np.float32)
+    tmax = (tmin + rng.uniform(0.0, 4.0, size=n)).astype(np.float32)
+    assert_hits_equal(gpu_isect(backend, o, d, tmin, tmax), oracle_bvh.intersect(o, d, tmin, tmax))
+    rays = sptamd.Ray3.make(o, d)
+    init = (77, 5.0, 6.0, 7.0)
+    for mask in (np.zeros(1, np.uint8), np.ones(1, np.uint8), (np.arange(n) % 3 != 0).astype(np.uint8)):
+        out = (torch.full((n,), 77, dtype=torch.int32, device="cuda"),) + tuple(
+            torch.full((n,), x, device="cuda") for x in init[1:])
+        backend.intersect_raw(rays, mask=mask, out=out)
+        torch.cuda.synchronize()
+        full = mask if mask.size == n else np.full(n, mask[0], np.uint8)
+        r = oracle_bvh.intersect(o, d, mask=full, init=[np.full(n, 77, np.int32)] +
+                                 [np.full(n, x, np.float32) for x in init[1:]])
+        got = [g.cpu().numpy() for g in out]
+        np.testing.assert_array_equal(got[0], r[0])
+        np.testing.assert_array_equal(got[1], r[1])
+        h = r[0] >= 0
+        np.testing.assert_array_equal(got[2][h], r[2][h])
+        np.testing.assert_array_equal(got[3][h], r[3][h])
