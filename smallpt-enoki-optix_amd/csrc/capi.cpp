@@ -784,7 +784,6 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         S.sc = sc->dev();
         S.hits = (const float4*)b.hits;
         S.sfilm = sfilm;
-        S.stats = ws.stats->stats;
         S.P = (uint32_t)P; S.W = p.width; S.max_depth = p.max_depth;
         S.xcd_remap = (env_u32("SPT_XCD", 3, 0, 3) >> 1) & 1u;
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
@@ -855,6 +854,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = nullptr; ra[k].cursor_init = wb;
             ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];
             ra[k].surv_clear = nullptr;
+            ra[k].casts_in = nullptr;
             const uint32_t first = (uint32_t)std::min<uint64_t>(b.cap, we - wb);
             sub_end[k] = we;
             started[k] = wb + first;
@@ -913,6 +913,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
                     ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
                     ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
                     ra[k].surv_clear = &b.cnt->surv[c];
+                    ra[k].casts_in = &b.cnt->qn[c];
                     // new paths: at most the work not yet known to be started (one
                     // block still runs to carry the counters over)
                     const uint32_t fill = (uint32_t)std::min<uint64_t>(b.cap, sub_end[k] - started[k]);

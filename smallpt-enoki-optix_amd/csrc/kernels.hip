@@ -678,6 +678,11 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         *a.qn_out = surv + total;
         *a.isect_next = 0;
         if (a.surv_clear) *a.surv_clear = 0;
+        if (a.casts_in) {  // the shade before: its queue count and its survivors
+            const uint32_t casts = *a.casts_in;
+            if (casts) atomicAdd(&a.stats[0], (unsigned long long)casts);
+            if (surv) atomicAdd(&a.stats[1], (unsigned long long)surv);
+        }
         if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
     }
     if (i >= total) return;
@@ -709,14 +714,12 @@ template <bool kEmit>
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
-    __shared__ uint32_t s_stats[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = *a.count_in;
     // the grid may be sized from a stale (larger) count: remap only the
     // blocks that hold queued paths, so every XCD gets its eighth of them
     const uint32_t nreal = min(gridDim.x, (n + kShadeBlock - 1) / kShadeBlock);
     const uint32_t i = (a.xcd_remap && blockIdx.x < nreal ? xcd_block(blockIdx.x, nreal) : blockIdx.x) * kShadeBlock + tid;
-    if (tid < 2) s_stats[tid] = 0;
 
     // ---- phase 1: survive or terminate (the bounce inputs load alongside)
     bool emit = false;
@@ -789,26 +792,18 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
     }
 
-    // ---- compaction: wave ballot + mbcnt rank, one queue atomic per block
+    // ---- compaction: wave ballot + mbcnt rank, one queue atomic per block.
+    // (Casts and continuations are the queue counts: the refill that follows
+    // adds them to the stats, so no per-block stats atomics contend here.)
     const uint64_t ball = __ballot(emit);
     const uint32_t rank =
         __builtin_amdgcn_mbcnt_hi((uint32_t)(ball >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ball, 0u));
-    const uint64_t bi = __ballot(i < n);
-    __syncthreads();  // s_stats initialised
-    if (lane == 0) {
-        s_wave_cnt[wave] = (uint32_t)__popcll(ball);
-        atomicAdd(&s_stats[0], (uint32_t)__popcll(bi));
-        atomicAdd(&s_stats[1], (uint32_t)__popcll(ball));
-    }
+    if (lane == 0) s_wave_cnt[wave] = (uint32_t)__popcll(ball);
     __syncthreads();
     uint32_t base = 0, total = 0;
     if (tid == 0) {
         for (uint32_t w = 0; w < kShadeBlock / 64; w++) total += s_wave_cnt[w];
         if (total) base = atomicAdd(a.count_out, total);  // returns during phase 2
-        if (s_stats[0]) {
-            atomicAdd(&a.stats[0], (unsigned long long)s_stats[0]);
-            if (s_stats[1]) atomicAdd(&a.stats[1], (unsigned long long)s_stats[1]);
-        }
     }
 
     // ---- phase 2: the bounce ray of every survivor

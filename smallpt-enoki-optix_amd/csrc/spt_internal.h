@@ -93,7 +93,6 @@ struct ShadeArgs {
     const uint32_t* count_in;
     uint32_t* count_out;        // survivors appended here (zeroed before the launch)
     float* sfilm;               // [spp_chunk][3][P]: one contribution per (sample, pixel)
-    unsigned long long* stats;  // casts, continuations, regenerations
     uint32_t P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     float env_r, env_g, env_b;
@@ -112,8 +111,10 @@ struct RefillArgs {
     uint32_t* qn_out;           // queue count for the next isect, thread 0 only
     uint32_t* isect_next;       // zeroed by thread 0 for the next isect launch
     uint32_t* surv_clear;       // zeroed by thread 0: the next shade's survivor counter (may be null)
+    const uint32_t* casts_in;   // the preceding shade's queue count (null for a chunk's first refill):
+                                // thread 0 adds it and *surv to stats[0] / stats[1]
     const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
-    unsigned long long* stats;
+    unsigned long long* stats;  // casts, continuations, regenerations
     uint64_t work_end;          // W_total (work items of this chunk end here)
     uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
