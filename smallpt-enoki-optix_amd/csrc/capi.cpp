@@ -677,9 +677,13 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     if (!film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
 
     // Wavefront capacity.  Each isect launch ends in a tail where its last rays
-    // finish while most lanes idle; 8M paths in flight (~1 GB of queues)
-    // amortise it (measured: 1M 913, 2M 1191, 8M 1792 Mpaths/s on MI355X).
-    uint64_t C = p.wavefront_paths ? p.wavefront_paths : (1ull << 23);
+    // finish while most lanes idle, and every iteration pays launch gaps and a
+    // shade + refill during which its stream's share of the chip is not
+    // tracing; 32M paths in flight (~5 GB of queues: HBM is 288 GB) amortise
+    // both.  Config 1, Mpaths/s: 8M 3235, 12M 3470, 16M 3463, 24M 3755,
+    // 32M 3715, 48M 3722; configs 2 / 3 / 4: 8M 1712 / 3824 / 851 against
+    // 32M 1790 / 4080 / 860.
+    uint64_t C = p.wavefront_paths ? p.wavefront_paths : (1ull << 25);
 
     // Pipeline: the wavefront (isect / shade / refill over path queues, the
     // north-star design) or the fused persistent kernel (bit-identical).  The
@@ -691,7 +695,10 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // Traversal counters exist in the wavefront isect kernel only.
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
     const uint32_t fused_env = env_u32("SPT_FUSED", 2, 0, 2);
-    bool fused = fused_env == 2 ? P * p.spp <= C : fused_env == 1;
+    // the job-size rule was measured against an 8M-path wavefront (the fused
+    // kernel's crossover); an explicit wavefront size moves it with it
+    const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : (1ull << 23);
+    bool fused = fused_env == 2 ? P * p.spp <= fused_max : fused_env == 1;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
     if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
