@@ -781,8 +781,10 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         I.max_depth = p.max_depth;
         I.trav_stats = trav_stats ? ws.stats->trav : nullptr;
         I.next = &b.cnt->isect_next;
-        I.refill_idle = env_u32("SPT_REFILL_IDLE", kRefillIdle, 1, 64);
-        I.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 160, 0, 255);
+        // 24 idle lanes / a 1/2 static share: +1.5 % over 16 / 5/8 at the
+        // 32M wavefront (tools/envsweep.sh, tools/envsweep_r01_v11.txt)
+        I.refill_idle = env_u32("SPT_REFILL_IDLE", 24, 1, 64);
+        I.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 128, 0, 255);
         I.xcd_remap = env_u32("SPT_XCD", 3, 0, 3) & 1u;
         I.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
         // each stream's persistent grid covers 1/K of the chip (measured best)
