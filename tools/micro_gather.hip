@@ -53,6 +53,47 @@ __global__ __launch_bounds__(256) void gather(const float4* __restrict__ table, 
     if (acc.x == 1234.5f) out[0] = acc;  // keep the loads
 }
 
+// kq quads per lane from the lane's own random 128-B line (a node fetch):
+// is the cost per wave-instruction or per line?
+template <int kq>
+__global__ __launch_bounds__(256) void node_fetch(const float4* __restrict__ table, uint32_t lines_mask, int iters,
+                                                  float4* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    float4 acc = make_float4(0, 0, 0, 0);
+    uint32_t seed = hash(wave * 9781u + 17u);
+    for (int it = 0; it < iters; it++) {
+        const uint32_t line = hash(seed + lane * 131u) & lines_mask;
+        const float4* p = table + line * 8u;
+        float4 v[kq];
+#pragma unroll
+        for (int j = 0; j < kq; j++) v[j] = p[j];
+#pragma unroll
+        for (int j = 0; j < kq; j++) { acc.x += v[j].x; acc.y += v[j].y; acc.z += v[j].z; acc.w += v[j].w; }
+        seed = hash(seed + (uint32_t)it);
+    }
+    if (acc.x == 1234.5f) out[0] = acc;
+}
+
+template <int kq>
+static int time_node(const float4* d_t, uint32_t mask, float4* d_o, hipEvent_t e0, hipEvent_t e1) {
+    const int iters = 256, blocks = 256 * 8;
+    for (int rep = 0; rep < 2; rep++) {
+        CHECK(hipEventRecord(e0));
+        hipLaunchKernelGGL(node_fetch<kq>, dim3(blocks), dim3(256), 0, 0, d_t, mask, iters, d_o);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        const double fetches = (double)blocks * 4 * iters;  // wave-level node fetches
+        if (rep)
+            std::printf("{\"node_quads\": %d, \"table_lines\": %u, \"ms\": %.3f, \"ns_per_fetch_per_cu\": %.2f, "
+                        "\"ns_per_inst_per_cu\": %.2f}\n", kq, mask + 1, ms, ms * 1e6 / (fetches / 256.0),
+                        ms * 1e6 / (fetches * kq / 256.0));
+    }
+    return 0;
+}
+
 int main() {
     const uint32_t kLines = 16384;  // 2 MiB table, L2-resident
     std::vector<float4> h(kLines * 8);
@@ -88,6 +129,18 @@ int main() {
                                 ms * 1e6 / (insts / 256.0));
             }
         }
+    }
+    // node fetches: L2-resident (2 MiB) and beyond L2 (256 MiB, like the 26-MB scene x lines)
+    const uint32_t big = 1u << 21;  // 2M lines = 256 MiB
+    float4* d_big;
+    CHECK(hipMalloc(&d_big, (size_t)big * 8 * sizeof(float4)));
+    CHECK(hipMemset(d_big, 0, (size_t)big * 8 * sizeof(float4)));
+    for (uint32_t mask : {kLines - 1u, big - 1u}) {
+        const float4* t = mask == kLines - 1u ? d_t : d_big;
+        if (time_node<1>(t, mask, d_o, e0, e1) || time_node<2>(t, mask, d_o, e0, e1) ||
+            time_node<3>(t, mask, d_o, e0, e1) || time_node<4>(t, mask, d_o, e0, e1) ||
+            time_node<5>(t, mask, d_o, e0, e1) || time_node<8>(t, mask, d_o, e0, e1))
+            return 1;
     }
     return 0;
 }
