@@ -803,7 +803,13 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     uint32_t base = 0, total = 0;
     if (tid == 0) {
         for (uint32_t w = 0; w < kShadeBlock / 64; w++) total += s_wave_cnt[w];
-        if (total) base = atomicAdd(a.count_out, total);  // returns during phase 2
+        // returns during phase 2.  The address goes through an opaque VGPR
+        // zero: for a uniform address the compiler's atomic optimizer wraps
+        // the add in a wave scan whose readfirstlane waits for the return
+        // right here, serialising the atomic's latency with phase 2.
+        uint32_t zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+        if (total) base = atomicAdd(a.count_out + zero, total);
     }
 
     // ---- phase 2: the bounce ray of every survivor
