@@ -695,9 +695,11 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // Traversal counters exist in the wavefront isect kernel only.
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
     const uint32_t fused_env = env_u32("SPT_FUSED", 2, 0, 2);
-    // the job-size rule was measured against an 8M-path wavefront (the fused
-    // kernel's crossover); an explicit wavefront size moves it with it
-    const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : (1ull << 23);
+    // the job-size rule: the fused kernel up to 16M paths (config 1 tiles:
+    // 1/4 fused 3559 vs wavefront 3224, 1/8 3078 vs 2448 Mpaths/s; whole
+    // image 3848 vs 3823, within noise, so the wavefront keeps large jobs);
+    // an explicit wavefront size moves the rule with it
+    const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : (1ull << 24);
     bool fused = fused_env == 2 ? P * p.spp <= fused_max : fused_env == 1;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
     if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
@@ -823,7 +825,10 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
         F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
         F.refill_idle = env_u32("SPT_FUSED_IDLE", 32, 1, 64);
-        F.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 160, 0, 255);
+        // a small static share: the fused lanes' path lengths vary far more
+        // than one cast's, so most work is taken dynamically (1/8 tile of
+        // config 1: 32/256 3006, 0: 2938, 64: 2912, 160: 2558 Mpaths/s)
+        F.static_share_q8 = env_u32("SPT_FUSED_STATIC_SHARE_Q8", 32, 0, 255);
         F.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
         F.grid_q8 = env_u32("SPT_FUSED_GRID_Q8", 256, 0, 4096);
         F.env_r = p.env[0]; F.env_g = p.env[1]; F.env_b = p.env[2];
