@@ -262,3 +262,22 @@ def test_fused_emission_and_tiles(cornell):
         tile, _ = gpu_render(s, 48, 40, 8, 10, tile_index=t, tile_count=3, rows_per_group=4, pipeline="fused", **kw)
         img[:, rows, :] = tile
     np.testing.assert_array_equal(img, ref)
+
+
+@pytest.mark.parametrize("env", [
+    {"SPT_STATIC_SHARE_Q8": "0", "SPT_REFILL_IDLE": "1"},
+    {"SPT_STATIC_SHARE_Q8": "255", "SPT_REFILL_IDLE": "64", "SPT_CHUNK": "1"},
+    {"SPT_STREAMS": "3", "SPT_ISECT_GRID_Q8": "16", "SPT_XCD": "0"},
+    {"SPT_FUSED_STATIC_SHARE_Q8": "255", "SPT_FUSED_IDLE": "1"},
+    {"SPT_FUSED_STATIC_SHARE_Q8": "0", "SPT_FUSED_IDLE": "64", "SPT_CHUNK": "7", "SPT_FUSED_GRID_Q8": "8"},
+])
+def test_scheduling_knobs_invariance(gscene, oscene, monkeypatch, env):
+    """The work-distribution knobs (static/dynamic shares, refill thresholds,
+    stream count, grid sizes) change only which lane traces which path: both
+    pipelines must still produce the oracle's film bit for bit."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    got, st = gpu_render(gscene, 48, 40, 7, 4, wavefront_paths=3000)
+    ref, casts = oracle_render(oscene, 48, 40, 7, 4)
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
