@@ -48,8 +48,9 @@ typedef struct spt_hits {
 } spt_hits;
 
 /* Reconstructed surface — optix_backend.h:99-134 (TriangleHitInfo) plus the
- * material id gathered by Scene::intersect (main.cpp:325).  Each pointer may be
- * NULL to skip that output.  Planar SoA, n elements per plane. */
+ * material id gathered by Scene::intersect (main.cpp:325).  Each plane pointer
+ * may be NULL on its own to skip that output (e.g. px alone).  Planar SoA, n
+ * elements per plane. */
 typedef struct spt_hit_info {
     float* px; float* py; float* pz;          /* position o + t d          (:469)     */
     float* gnx; float* gny; float* gnz;       /* geometric normal          (:472-476) */
@@ -79,8 +80,9 @@ enum {
     SPT_FLAG_TRAVERSAL_STATS = 2u, /* count node visits / triangle tests (slower variant; wavefront) */
     SPT_FLAG_FUSED = 4u,           /* one persistent trace+shade kernel per sample chunk */
     SPT_FLAG_WAVEFRONT = 8u,       /* isect / shade / refill kernels over path queues
-                                      (neither flag: env SPT_FUSED, else fused iff the job
-                                      is at most two wavefronts of paths) */
+                                      (neither flag: spt_config.pipeline; AUTO = fused iff
+                                      the tile has at most fused_max_paths = 16M paths, or
+                                      at most wavefront_paths when that is set) */
     SPT_FLAG_TIMING_ALL = 16u      /* with SPT_FLAG_TIMING: also shade / refill / resolve launches */
 };
 
@@ -93,7 +95,7 @@ typedef struct spt_render_params {
     /* Interleaved row-group tiling: global row r belongs to tile
      * (r / rows_per_group) % tile_count.  tile_count = 1 renders the image. */
     uint32_t tile_index, tile_count, rows_per_group;
-    uint32_t wavefront_paths;   /* paths in flight per launch (0 = auto: 8M) */
+    uint32_t wavefront_paths;   /* paths in flight per launch (0 = the scene's config: 32M) */
     uint32_t rr_start_depth;    /* Russian roulette from this cast on (>= max_depth: off) */
     uint32_t rng_order;         /* SPT_RNG_* */
     uint64_t rng_initstate;     /* PCG32_DEFAULT_STATE 0x853c49e6748fea9b (main.cpp:376) */
@@ -116,7 +118,7 @@ typedef struct spt_render_stats {
     uint64_t isect_lane_steps;  /*   traversal loop iterations summed over lanes */
     uint64_t isect_wave_steps;  /*   traversal loop iterations summed over waves */
     uint64_t isect_launches;    /* SPT_FLAG_TIMING: isect launches timed (all streams) */
-    uint32_t streams;           /* sub-wavefronts (HIP streams) used, env SPT_STREAMS */
+    uint32_t streams;           /* sub-wavefronts (HIP streams) used (spt_config.streams) */
     uint32_t fused;             /* 1: the fused pipeline ran, 0: the wavefront */
     double isect_busy_ms;       /* SPT_FLAG_TIMING: union of the isect launch intervals
                                    (launches on the K streams overlap; isect_ms sums them) */
@@ -127,7 +129,7 @@ typedef struct spt_scene_stats {
     uint64_t ntri, nodes, leaves;
     uint32_t max_depth;         /* BVH depth (sets the LDS stack depth) */
     uint32_t max_leaf;
-    uint32_t bvh_width;         /* 8: compressed 8-wide BVH (default), 2: BVH2 (env SPT_BVH=2) */
+    uint32_t bvh_width;         /* 8: compressed 8-wide BVH (default), 2: BVH2 (spt_config.bvh_width) */
     uint32_t builder;           /* SPT_BUILD_HOST_SAH or SPT_BUILD_GPU_PLOC: the build that ran */
     uint64_t device_bytes;
     double build_ms;            /* BVH build (host SAH, or GPU PLOC + collapse, synchronised) */
@@ -166,7 +168,7 @@ spt_status spt_scene_create(const int32_t* pos_tri, const float* pos, uint64_t n
  * optix_backend.h:336-358).  Both give the compressed 8-wide BVH; closest
  * hits do not depend on the tree (ties go to the smaller triangle id). */
 typedef enum spt_build {
-    SPT_BUILD_AUTO = 0,         /* env SPT_BUILD=host|gpu, else GPU from 2M triangles up */
+    SPT_BUILD_AUTO = 0,         /* GPU from spt_config.gpu_build_min_tris (2M) triangles up */
     SPT_BUILD_HOST_SAH = 1,     /* binned-SAH BVH2 on the host threads, collapsed on the host */
     SPT_BUILD_GPU_PLOC = 2      /* PLOC BVH2 + collapse on the GPU (gpu_build.hip) */
 } spt_build;
@@ -176,6 +178,58 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
                                const int32_t* nrm_tri, const float* nrm, uint64_t nnrm,
                                const int32_t* tc_tri, const float* tc, uint64_t ntc,
                                const int32_t* mat_id, uint32_t build, spt_scene* out);
+
+/* Tuning and build knobs of one scene.  The library reads no environment
+ * variables: every knob is here (the Python host maps its SPT_* variables onto
+ * these fields as overrides).  spt_default_config fills the measured defaults
+ * (DESIGN.md §4); spt_scene_set_config validates ranges and returns
+ * SPT_ERR_INVALID for a value outside them.  Build fields are read only by
+ * spt_scene_create_cfg; render / intersect fields by every later call. */
+enum {
+    SPT_PIPELINE_AUTO = 0,      /* fused iff W*H*spp of the tile <= fused_max_paths */
+    SPT_PIPELINE_WAVEFRONT = 1, /* isect / shade / refill over path queues */
+    SPT_PIPELINE_FUSED = 2      /* one persistent trace+shade kernel per sample chunk */
+};
+typedef struct spt_config {
+    /* --- scene build (spt_scene_create_cfg) */
+    uint32_t build;                 /* spt_build (AUTO: GPU from gpu_build_min_tris up)      [0..2] */
+    uint32_t bvh_width;             /* 8: compressed BVH8 (default), 2: BVH2 (host build)   {2, 8} */
+    uint64_t gpu_build_min_tris;    /* SPT_BUILD_AUTO threshold, 2,000,000                          */
+    uint32_t collapse;              /* BVH8 collapse: 0 SAH-optimal DP (default), 1 greedy    [0..1] */
+    uint32_t ploc_radius;           /* GPU PLOC search radius                        {8, 16, 32, 64} */
+    uint32_t stack_slack;           /* extra LDS stack entries per lane (0)                  [0..64] */
+    /* --- spt_render */
+    uint32_t pipeline;              /* SPT_PIPELINE_* (the params' FUSED / WAVEFRONT flags win) [0..2] */
+    uint64_t fused_max_paths;       /* AUTO rule: fused for tiles of <= this many paths, 2^24       */
+    uint32_t wavefront_paths;       /* paths in flight when params.wavefront_paths == 0, 2^25 [1..2^31) */
+    uint32_t streams;               /* sub-wavefronts (HIP streams) of the wavefront, 4      [1..4] */
+    uint32_t isect_refill_idle;     /* refill a wave once this many lanes are idle, 24       [1..64] */
+    uint32_t isect_static_share_q8; /* static share of the queue per wave, 128/256          [0..255] */
+    uint32_t isect_chunk;           /* queue indices per dynamic grab, 128                 [1..4096] */
+    uint32_t isect_grid_q8;         /* persistent grid per stream in 1/256 chip, 0 = 256/streams [0..4096] */
+    uint32_t xcd_remap;             /* bit 0: isect, bit 1: shade XCD-aware block numbering, 3 [0..3] */
+    uint32_t fused_refill_idle;     /* fused kernel: shade/refill once this many lanes idle, 32 [1..64] */
+    uint32_t fused_static_share_q8; /* fused kernel static share, 32/256                    [0..255] */
+    uint32_t fused_grid_q8;         /* fused grid in 1/256 of the chip, 256                [0..4096] */
+    uint32_t plane_pad;             /* path-queue plane padding (elements), 0            [0..2^20] */
+    uint64_t film_budget_bytes;     /* per-sample film chunk budget (4 GiB): smaller values
+                                       split the samples into more chunks            [>= 12 x tile px] */
+    /* --- spt_intersect */
+    uint32_t public_persistent;     /* 1: lane-refill persistent kernel, 0: one lane per ray  [0..1] */
+    uint32_t public_refill_idle;    /* its refill threshold, 16                              [1..64] */
+} spt_config;
+
+void spt_default_config(spt_config* cfg);
+
+/* spt_scene_create with a configuration (NULL = spt_default_config). */
+spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                                const int32_t* nrm_tri, const float* nrm, uint64_t nnrm,
+                                const int32_t* tc_tri, const float* tc, uint64_t ntc,
+                                const int32_t* mat_id, const spt_config* cfg, spt_scene* out);
+
+/* Replace / read the scene's configuration (the build fields are kept as built). */
+spt_status spt_scene_set_config(spt_scene scene, const spt_config* cfg);
+spt_status spt_scene_get_config(spt_scene scene, spt_config* out);
 
 /* Per-material albedo (RGB, nmat x 3).  Default: 1 for every material, as in
  * the reference (main.cpp:234,244 — Kd is read and discarded). */
@@ -208,7 +262,11 @@ spt_status spt_hit_info_compute(spt_scene scene, const spt_rays* rays, const spt
 /* main.cpp:354-429: the whole wavefront render of one tile.  film_dev is a
  * device buffer of 3 x tile_rows x width floats (planar R, G, B as the
  * reference's SpectrumC film, main.cpp:369), already divided by spp.  The
- * call returns after the stream has drained.  stats may be NULL. */
+ * call returns after the stream has drained.  stats may be NULL.
+ * Threading: a scene owns one render workspace (path queues, film chunks,
+ * events), so spt_render calls on one scene are serialised by a per-scene
+ * mutex (a second thread waits); render concurrently from one scene per
+ * thread / device.  spt_scene_set_config takes the same mutex. */
 spt_status spt_render(spt_scene scene, const spt_render_params* params, float* film_dev,
                       spt_render_stats* stats, void* stream);
 

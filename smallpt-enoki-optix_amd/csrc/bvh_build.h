@@ -47,6 +47,7 @@ struct Bvh8BuildResult {
     uint64_t leaves = 0;
     double sah_cost = 0.0;           // of the underlying BVH2
 };
-Bvh8BuildResult build_bvh8(const float* tri_verts, uint64_t ntri);
+// greedy: the greedy collapse instead of the SAH-optimal dynamic program.
+Bvh8BuildResult build_bvh8(const float* tri_verts, uint64_t ntri, bool greedy = false);
 
 }  // namespace spt

@@ -10,6 +10,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -49,14 +50,6 @@ void hfree(T*& p) {
     p = nullptr;
 }
 
-// Tuning knobs read from the environment (defaults are the measured best).
-uint32_t env_u32(const char* name, uint32_t dflt, uint32_t lo, uint32_t hi) {
-    const char* v = std::getenv(name);
-    if (!v || !*v) return dflt;
-    long x = std::strtol(v, nullptr, 10);
-    return (uint32_t)std::max<long>(lo, std::min<long>(hi, x));
-}
-
 double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -78,12 +71,9 @@ PathQueue carve_queue(char* base, size_t stride) {
     return q;
 }
 
-// Plane stride: cap plus a pad so the SoA planes (and the two queues) do not
-// sit a power of two apart.
-size_t queue_stride(size_t cap) {
-    static const uint32_t pad = env_u32("SPT_PLANE_PAD", 0, 0, 1u << 20);
-    return cap + pad;
-}
+// Plane stride: cap plus a pad (spt_config.plane_pad) so the SoA planes (and
+// the two queues) need not sit a power of two apart.
+size_t queue_stride(size_t cap, uint32_t pad) { return cap + pad; }
 
 // Device counters of one sub-wavefront (zeroed per chunk; see spt_render).
 struct Counters {
@@ -106,6 +96,7 @@ constexpr int kMaxStreams = 4;
 // counters, driven on its own stream so its launch tails overlap the others'.
 struct Sub {
     size_t cap = 0;
+    uint32_t pad = 0;                   // plane pad the queues were carved with
     char* qa = nullptr;
     char* qb = nullptr;
     char* hits = nullptr;
@@ -145,6 +136,8 @@ struct Workspace {
 
 struct spt_scene_t {
     int device = 0;
+    spt_config cfg{};
+    std::mutex mu;  // one workspace per scene: spt_render / spt_scene_set_config serialise here
     uint64_t ntri = 0;
     float4* nodes = nullptr;
     uint4* nodes8 = nullptr;
@@ -213,16 +206,17 @@ Camera make_camera(const spt_render_params& p) {
     return cam;
 }
 
-spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, size_t film_floats, size_t njumps) {
+spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, size_t film_floats, size_t njumps) {
     for (int k = 0; k < nsub; k++) {
         Sub& b = ws.sub[k];
-        if (cap > b.cap) {
+        if (cap > b.cap || pad != b.pad) {
             hfree(b.qa); hfree(b.qb); hfree(b.hits);
             b.cap = 0;
-            HIP_TRY(hipMalloc((void**)&b.qa, kPathBytes * queue_stride(cap)));
-            HIP_TRY(hipMalloc((void**)&b.qb, kPathBytes * queue_stride(cap)));
+            HIP_TRY(hipMalloc((void**)&b.qa, kPathBytes * queue_stride(cap, pad)));
+            HIP_TRY(hipMalloc((void**)&b.qb, kPathBytes * queue_stride(cap, pad)));
             HIP_TRY(hipMalloc((void**)&b.hits, kHitBytes * cap));
             b.cap = cap;
+            b.pad = pad;
         }
         if (!b.cnt) HIP_TRY(hipMalloc((void**)&b.cnt, sizeof(Counters)));
         if (!b.host_cnt) HIP_TRY(hipHostMalloc((void**)&b.host_cnt, 2 * sizeof(Counters), hipHostMallocDefault));
@@ -263,20 +257,48 @@ spt_status get_event(Workspace& ws, size_t idx, hipEvent_t* out) {
 // Tracer8 pushes the group of node X (level L) only when descending into one
 // of X's inner children (level L + 1 <= depth), and the stack then holds one
 // group per node on the path root..X: at most depth - 1 entries.  A tight
-// stack is LDS, and LDS sets the occupancy (env SPT_STACK_SLACK adds entries).
-uint32_t bvh8_stack_entries(uint32_t depth) {
-    static const uint32_t slack = env_u32("SPT_STACK_SLACK", 0, 0, 64);
+// stack is LDS, and LDS sets the occupancy (spt_config.stack_slack adds entries).
+uint32_t bvh8_stack_entries(uint32_t depth, uint32_t slack) {
     return std::max<uint32_t>(1, depth > 1 ? depth - 1 + slack : 1 + slack);
 }
 
-// Triangle count from which SPT_BUILD_AUTO builds on the GPU.
-constexpr uint64_t kGpuBuildAutoTris = 2000000;
+// Range checks of spt_scene_set_config / spt_scene_create_cfg.
+spt_status check_config(const spt_config& c) {
+#define CFG_RANGE(f, lo, hi)                                                                         \
+    if ((uint64_t)c.f < (uint64_t)(lo) || (uint64_t)c.f > (uint64_t)(hi))                           \
+        return fail(SPT_ERR_INVALID, "spt_config.%s = %llu outside [%llu, %llu]", #f, (unsigned long long)c.f, \
+                    (unsigned long long)(lo), (unsigned long long)(hi));
+    CFG_RANGE(build, 0, SPT_BUILD_GPU_PLOC)
+    if (c.bvh_width != 2 && c.bvh_width != 8) return fail(SPT_ERR_INVALID, "spt_config.bvh_width must be 2 or 8");
+    CFG_RANGE(collapse, 0, 1)
+    if (c.ploc_radius != 8 && c.ploc_radius != 16 && c.ploc_radius != 32 && c.ploc_radius != 64)
+        return fail(SPT_ERR_INVALID, "spt_config.ploc_radius must be 8, 16, 32 or 64");
+    CFG_RANGE(stack_slack, 0, 64)
+    CFG_RANGE(pipeline, 0, SPT_PIPELINE_FUSED)
+    CFG_RANGE(wavefront_paths, 1, 0x7fffffffu)
+    CFG_RANGE(streams, 1, kMaxStreams)
+    CFG_RANGE(isect_refill_idle, 1, 64)
+    CFG_RANGE(isect_static_share_q8, 0, 255)
+    CFG_RANGE(isect_chunk, 1, 4096)
+    CFG_RANGE(isect_grid_q8, 0, 4096)
+    CFG_RANGE(xcd_remap, 0, 3)
+    CFG_RANGE(fused_refill_idle, 1, 64)
+    CFG_RANGE(fused_static_share_q8, 0, 255)
+    CFG_RANGE(fused_grid_q8, 0, 4096)
+    CFG_RANGE(plane_pad, 0, 1u << 20)
+    CFG_RANGE(film_budget_bytes, 12, UINT64_MAX)
+    CFG_RANGE(public_persistent, 0, 1)
+    CFG_RANGE(public_refill_idle, 1, 64)
+#undef CFG_RANGE
+    return SPT_OK;
+}
 
 // spt_scene_create on the GPU: upload the indexed mesh as is, assemble the
 // triangle soup, PLOC + collapse (gpu_build.hip), slot-ordered arrays.
 spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
                             const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
-                            const float* tc, uint64_t ntc, const int32_t* mat_id, double t0, spt_scene* out) {
+                            const float* tc, uint64_t ntc, const int32_t* mat_id, const spt_config& cfg, double t0,
+                            spt_scene* out) {
     struct Raw {
         int32_t *pt = nullptr, *nt = nullptr, *tt = nullptr, *mat = nullptr;
         float *p = nullptr, *n = nullptr, *t = nullptr, *tv = nullptr;
@@ -297,11 +319,12 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     hipStream_t s = nullptr;  // the null stream: scene creation is synchronous
     HIP_TRY(gpu_mesh_soup(m, raw.tv, s));
     GpuBvh8 g;
-    HIP_TRY(gpu_build_bvh8(raw.tv, (uint32_t)ntri, s, &g));
+    HIP_TRY(gpu_build_bvh8(raw.tv, (uint32_t)ntri, s, &g, (int)cfg.ploc_radius, cfg.collapse == 1));
     spt_scene_t* sc = new spt_scene_t();
+    sc->cfg = cfg;
     (void)hipGetDevice(&sc->device);
     sc->ntri = ntri;
-    sc->stack_depth = bvh8_stack_entries(g.depth);
+    sc->stack_depth = bvh8_stack_entries(g.depth, cfg.stack_slack);
     uint32_t nslots = 0;
     {
         uint32_t* holes = nullptr;
@@ -422,22 +445,32 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
                                const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
                                const float* tc, uint64_t ntc, const int32_t* mat_id, uint32_t build,
                                spt_scene* out) {
+    if (build > SPT_BUILD_GPU_PLOC) return fail(SPT_ERR_INVALID, "spt_scene_create: unknown builder %u", build);
+    spt_config cfg;
+    spt_default_config(&cfg);
+    cfg.build = build;
+    return spt_scene_create_cfg(pos_tri, pos, nvert, ntri, nrm_tri, nrm, nnrm, tc_tri, tc, ntc, mat_id, &cfg, out);
+}
+
+spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64_t nvert, uint64_t ntri,
+                                const int32_t* nrm_tri, const float* nrm, uint64_t nnrm, const int32_t* tc_tri,
+                                const float* tc, uint64_t ntc, const int32_t* mat_id, const spt_config* cfg_in,
+                                spt_scene* out) {
     if (!out) return fail(SPT_ERR_INVALID, "spt_scene_create: out is NULL");
     *out = nullptr;
+    spt_config cfg;
+    if (cfg_in) cfg = *cfg_in;
+    else spt_default_config(&cfg);
+    spt_status st = check_config(cfg);
+    if (st) return st;
     if (ntri > 0 && (!pos_tri || !pos)) return fail(SPT_ERR_INVALID, "spt_scene_create: NULL positions");
     if (ntri >= kMaxTriangles) return fail(SPT_ERR_LIMIT, "spt_scene_create: %llu triangles exceeds 2^28", (unsigned long long)ntri);
     if (nrm_tri && !nrm && nnrm) return fail(SPT_ERR_INVALID, "spt_scene_create: normal indices without normals");
-    if (build > SPT_BUILD_GPU_PLOC) return fail(SPT_ERR_INVALID, "spt_scene_create: unknown builder %u", build);
-    spt_status st = ensure_device();
+    st = ensure_device();
     if (st) return st;
-    if (build == SPT_BUILD_AUTO) {
-        const char* b = std::getenv("SPT_BUILD");
-        if (b && std::strcmp(b, "gpu") == 0) build = SPT_BUILD_GPU_PLOC;
-        else if (b && std::strcmp(b, "host") == 0) build = SPT_BUILD_HOST_SAH;
-        else build = ntri >= kGpuBuildAutoTris ? SPT_BUILD_GPU_PLOC : SPT_BUILD_HOST_SAH;
-    }
-    const char* kind = std::getenv("SPT_BVH");
-    const bool use8 = !(kind && std::strcmp(kind, "2") == 0);
+    uint32_t build = cfg.build;
+    if (build == SPT_BUILD_AUTO) build = ntri >= cfg.gpu_build_min_tris ? SPT_BUILD_GPU_PLOC : SPT_BUILD_HOST_SAH;
+    const bool use8 = cfg.bvh_width == 8;
     if (build == SPT_BUILD_GPU_PLOC && !use8) build = SPT_BUILD_HOST_SAH;  // the GPU builder makes BVH8 only
     const double t0 = now_ms();
     const bool host = build == SPT_BUILD_HOST_SAH;
@@ -467,13 +500,13 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
             }
     }
     if (!host)
-        return create_scene_gpu(pos_tri, pos, nvert, ntri, nrm_tri, nrm, nnrm, tc_tri, tc, ntc, mat_id, t0, out);
-    // Acceleration structure: the compressed 8-wide BVH by default; SPT_BVH=2
-    // selects the plain BVH2 (kept as the simple reference layout).
+        return create_scene_gpu(pos_tri, pos, nvert, ntri, nrm_tri, nrm, nnrm, tc_tri, tc, ntc, mat_id, cfg, t0, out);
+    // Acceleration structure: the compressed 8-wide BVH by default;
+    // spt_config.bvh_width = 2 selects the plain BVH2 (the simple reference layout).
     BvhBuildResult bvh;
     Bvh8BuildResult bvh8;
     if (use8)
-        bvh8 = build_bvh8(tv.data(), ntri);
+        bvh8 = build_bvh8(tv.data(), ntri, cfg.collapse == 1);
     else
         bvh = build_bvh(tv.data(), ntri);
     const std::vector<uint32_t>& slot2tri = use8 ? bvh8.slot2tri : bvh.slot2tri;
@@ -511,9 +544,10 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
     }
 
     spt_scene_t* sc = new spt_scene_t();
+    sc->cfg = cfg;
     (void)hipGetDevice(&sc->device);
     sc->ntri = ntri;
-    sc->stack_depth = use8 ? bvh8_stack_entries(bvh8.depth) : std::max<uint32_t>(1, bvh.max_depth + 1);
+    sc->stack_depth = use8 ? bvh8_stack_entries(bvh8.depth, cfg.stack_slack) : std::max<uint32_t>(1, bvh.max_depth + 1);
     const float one[3] = {1.0f, 1.0f, 1.0f};
     spt_status us = SPT_OK;
     uint32_t nslots = 0;
@@ -592,6 +626,53 @@ spt_status spt_scene_set_emission(spt_scene sc, const float* emission_rgb, uint3
     return SPT_OK;
 }
 
+void spt_default_config(spt_config* c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->build = SPT_BUILD_AUTO;
+    c->bvh_width = 8;
+    c->gpu_build_min_tris = 2000000;
+    c->collapse = 0;
+    c->ploc_radius = 16;
+    c->stack_slack = 0;
+    c->pipeline = SPT_PIPELINE_AUTO;
+    c->fused_max_paths = 1ull << 24;
+    c->wavefront_paths = 1u << 25;
+    c->streams = 4;
+    c->isect_refill_idle = 24;
+    c->isect_static_share_q8 = 128;
+    c->isect_chunk = kIsectChunk;
+    c->isect_grid_q8 = 0;
+    c->xcd_remap = 3;
+    c->fused_refill_idle = 32;
+    c->fused_static_share_q8 = 32;
+    c->fused_grid_q8 = 256;
+    c->plane_pad = 0;
+    c->film_budget_bytes = 4ull << 30;
+    c->public_persistent = 0;
+    c->public_refill_idle = kRefillIdle;
+}
+
+spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
+    if (!sc || !cfg) return fail(SPT_ERR_INVALID, "spt_scene_set_config: NULL argument");
+    spt_status st = check_config(*cfg);
+    if (st) return st;
+    std::lock_guard<std::mutex> lk(sc->mu);
+    const spt_config old = sc->cfg;
+    sc->cfg = *cfg;
+    // the scene keeps the build it has
+    sc->cfg.build = old.build; sc->cfg.bvh_width = old.bvh_width; sc->cfg.gpu_build_min_tris = old.gpu_build_min_tris;
+    sc->cfg.collapse = old.collapse; sc->cfg.ploc_radius = old.ploc_radius; sc->cfg.stack_slack = old.stack_slack;
+    return SPT_OK;
+}
+
+spt_status spt_scene_get_config(spt_scene sc, spt_config* out) {
+    if (!sc || !out) return fail(SPT_ERR_INVALID, "spt_scene_get_config: NULL argument");
+    std::lock_guard<std::mutex> lk(sc->mu);
+    *out = sc->cfg;
+    return SPT_OK;
+}
+
 spt_status spt_scene_get_stats(spt_scene sc, spt_scene_stats* out) {
     if (!sc || !out) return fail(SPT_ERR_INVALID, "spt_scene_get_stats: NULL argument");
     *out = sc->stats;
@@ -623,7 +704,8 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
     a.n = n;
     a.closest = do_closest;
-    a.refill_idle = env_u32("SPT_PUBLIC_REFILL_IDLE", kRefillIdle, 1, 64);
+    a.refill_idle = sc->cfg.public_refill_idle;
+    a.persistent = sc->cfg.public_persistent;
     HIP_TRY(launch_isect_public(a, (hipStream_t)stream));
     return SPT_OK;
 }
@@ -632,6 +714,12 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
                                 uint32_t mask_size, uint32_t n, const spt_hit_info* out, void* stream) {
     if (!sc || !rays || !hits || !out) return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL argument");
     if (n == 0) return SPT_OK;
+    if (!hits->tri_id || !hits->t || !hits->u || !hits->v)
+        return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL hit plane");
+    // the rays are read only for the position (o + t d)
+    if ((out->px || out->py || out->pz) &&
+        (!rays->ox || !rays->oy || !rays->oz || !rays->dx || !rays->dy || !rays->dz))
+        return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL ray plane (needed for the position)");
     if (mask && mask_size != 1 && mask_size != n)
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: mask_size %u must be 1 or n=%u", mask_size, n);
     if (sc->ntri == 0) return SPT_OK;
@@ -675,6 +763,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         return SPT_OK;
     }
     if (!film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
+    std::lock_guard<std::mutex> lock(sc->mu);  // the scene's one workspace
+    const spt_config& cfg = sc->cfg;
 
     // Wavefront capacity.  Each isect launch ends in a tail where its last rays
     // finish while most lanes idle, and every iteration pays launch gaps and a
@@ -682,25 +772,24 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // tracing; 32M paths in flight (~5 GB of queues: HBM is 288 GB) amortise
     // both.  Config 1, Mpaths/s: 8M 3235, 12M 3470, 16M 3463, 24M 3755,
     // 32M 3715, 48M 3722; configs 2 / 3 / 4: 8M 1712 / 3824 / 851 against
-    // 32M 1790 / 4080 / 860.
-    uint64_t C = p.wavefront_paths ? p.wavefront_paths : (1ull << 25);
+    // 32M 1790 / 4080 / 860.  Default: spt_config.wavefront_paths = 32M.
+    uint64_t C = p.wavefront_paths ? p.wavefront_paths : cfg.wavefront_paths;
 
     // Pipeline: the wavefront (isect / shade / refill over path queues, the
     // north-star design) or the fused persistent kernel (bit-identical).  The
-    // flags choose; else env SPT_FUSED=0/1; else by job size: a job of at most
+    // flags choose; else spt_config.pipeline; else (AUTO) by job size: a job of at most
     // two wavefronts is mostly per-cast launch tails on the wavefront (queues
     // shrink cast by cast with no work left to refill them), where the fused
     // kernel's single tail wins — e.g. one rank's 1/8 of the headline image:
     // fused 2308 vs wavefront 1982 Mpaths/s; whole image: 2353 vs 2825.
     // Traversal counters exist in the wavefront isect kernel only.
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
-    const uint32_t fused_env = env_u32("SPT_FUSED", 2, 0, 2);
-    // the job-size rule: the fused kernel up to 16M paths (config 1 tiles:
-    // 1/4 fused 3559 vs wavefront 3224, 1/8 3078 vs 2448 Mpaths/s; whole
-    // image 3848 vs 3823, within noise, so the wavefront keeps large jobs);
-    // an explicit wavefront size moves the rule with it
-    const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : (1ull << 24);
-    bool fused = fused_env == 2 ? P * p.spp <= fused_max : fused_env == 1;
+    // the job-size rule: the fused kernel up to fused_max_paths = 16M paths
+    // (config 1 tiles: 1/4 fused 3559 vs wavefront 3224, 1/8 3078 vs 2448
+    // Mpaths/s; whole image 3848 vs 3823, within noise, so the wavefront keeps
+    // large jobs); an explicit wavefront size moves the rule with it
+    const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : cfg.fused_max_paths;
+    bool fused = cfg.pipeline == SPT_PIPELINE_AUTO ? P * p.spp <= fused_max : cfg.pipeline == SPT_PIPELINE_FUSED;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
     if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
@@ -710,15 +799,18 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // sub-wavefront's launch tail overlaps the others' work.
     // Measured on the headline config: 1 stream 1982, 2: 2649, 3: 2769, 4: 2791 Mpaths/s
     // (4 = the box's hardware queues per process, GPU_MAX_HW_QUEUES).
-    int K = fused ? 1 : (int)env_u32("SPT_STREAMS", 4, 1, kMaxStreams);
+    int K = fused ? 1 : (int)cfg.streams;
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
-    // Per-sample contribution film [chunk][3][P], at most ~4 GiB per chunk.
-    const uint64_t budget = 4ull << 30;
-    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(p.spp, budget / (12 * P)));
+    // Per-sample contribution film [chunk][3][P], at most film_budget_bytes
+    // (4 GiB) per chunk; chunks carry the running sum in acc.
+    const uint64_t budget = cfg.film_budget_bytes;
+    // (a chunk's work items are counted in 32 bits: at most 2^31 per chunk)
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (12 * P)), 0x7fffffffull / P));
     rs.paths_in_flight = (uint32_t)C;
-    spt_status st = ensure_workspace(sc->ws, K, Ck, (size_t)chunk * 3 * P + 3 * P, p.spp);
+    spt_status st = ensure_workspace(sc->ws, K, Ck, cfg.plane_pad, (size_t)chunk * 3 * P + 3 * P, p.spp);
     if (st) return st;
     Workspace& ws = sc->ws;
     // HIP events around the isect launches (the roofline kernel); every other
@@ -775,8 +867,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     PathQueue q[kMaxStreams][2];
     for (int k = 0; k < K; k++) {
         Sub& b = ws.sub[k];
-        q[k][0] = carve_queue(b.qa, queue_stride(b.cap));
-        q[k][1] = carve_queue(b.qb, queue_stride(b.cap));
+        q[k][0] = carve_queue(b.qa, queue_stride(b.cap, b.pad));
+        q[k][1] = carve_queue(b.qb, queue_stride(b.cap, b.pad));
         IsectQueueArgs& I = ia[k];
         I.sc = sc->dev();
         I.hits = (float4*)b.hits;
@@ -785,18 +877,18 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         I.next = &b.cnt->isect_next;
         // 24 idle lanes / a 1/2 static share: +1.5 % over 16 / 5/8 at the
         // 32M wavefront (tools/envsweep.sh, tools/envsweep_r01_v11.txt)
-        I.refill_idle = env_u32("SPT_REFILL_IDLE", 24, 1, 64);
-        I.static_share_q8 = env_u32("SPT_STATIC_SHARE_Q8", 128, 0, 255);
-        I.xcd_remap = env_u32("SPT_XCD", 3, 0, 3) & 1u;
-        I.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
+        I.refill_idle = cfg.isect_refill_idle;
+        I.static_share_q8 = cfg.isect_static_share_q8;
+        I.xcd_remap = cfg.xcd_remap & 1u;
+        I.chunk = cfg.isect_chunk;
         // each stream's persistent grid covers 1/K of the chip (measured best)
-        I.grid_q8 = env_u32("SPT_ISECT_GRID_Q8", 256u / (uint32_t)K, 0, 4096);
+        I.grid_q8 = cfg.isect_grid_q8 ? cfg.isect_grid_q8 : 256u / (uint32_t)K;
         ShadeArgs& S = sa[k];
         S.sc = sc->dev();
         S.hits = (const float4*)b.hits;
         S.sfilm = sfilm;
         S.P = (uint32_t)P; S.W = p.width; S.max_depth = p.max_depth;
-        S.xcd_remap = (env_u32("SPT_XCD", 3, 0, 3) >> 1) & 1u;
+        S.xcd_remap = (cfg.xcd_remap >> 1) & 1u;
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
         S.tile_index = p.tile_index; S.tile_count = p.tile_count; S.rows_per_group = p.rows_per_group;
         S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];
@@ -824,13 +916,13 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.P = (uint32_t)P; F.W = p.width; F.max_depth = p.max_depth;
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
         F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
-        F.refill_idle = env_u32("SPT_FUSED_IDLE", 32, 1, 64);
+        F.refill_idle = cfg.fused_refill_idle;
         // a small static share: the fused lanes' path lengths vary far more
         // than one cast's, so most work is taken dynamically (1/8 tile of
         // config 1: 32/256 3006, 0: 2938, 64: 2912, 160: 2558 Mpaths/s)
-        F.static_share_q8 = env_u32("SPT_FUSED_STATIC_SHARE_Q8", 32, 0, 255);
-        F.chunk = env_u32("SPT_CHUNK", kIsectChunk, 1, 4096);
-        F.grid_q8 = env_u32("SPT_FUSED_GRID_Q8", 256, 0, 4096);
+        F.static_share_q8 = cfg.fused_static_share_q8;
+        F.chunk = cfg.isect_chunk;
+        F.grid_q8 = cfg.fused_grid_q8;
         F.env_r = p.env[0]; F.env_g = p.env[1]; F.env_b = p.env[2];
         uint32_t lanes = 0;
         for (uint32_t s0 = 0; s0 < p.spp; s0 += chunk) {

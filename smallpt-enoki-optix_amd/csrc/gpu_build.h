@@ -19,7 +19,10 @@ struct GpuBvh8 {
 
 // d_tv: device, ntri x 9 floats (v0 v1 v2).  On success the caller owns
 // out->nodes8 and out->slot2tri (hipFree).  Synchronises stream s.
-hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out);
+// radius: PLOC search radius (8, 16, 32 or 64); greedy: greedy collapse
+// instead of the SAH-optimal one.
+hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out, int radius = 16,
+                          bool greedy = false);
 
 // Re-lays a compact BVH8 (both builders' output: nnodes nodes of kNode8Quads
 // quads, the inner children of a node contiguous from w4 in slot order) so

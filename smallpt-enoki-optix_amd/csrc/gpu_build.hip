@@ -28,7 +28,7 @@ namespace {
 
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kLeafMaxTris = 3;  // a BVH8 leaf holds up to 3 triangles
-constexpr int kDefaultRadius = 16;
+
 
 inline uint32_t blocks(uint64_t n, uint32_t b = kBlock) { return (uint32_t)((n + b - 1) / b); }
 
@@ -618,7 +618,7 @@ hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, ui
     return hipSuccess;
 }
 
-hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out) {
+hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out, int radius, bool greedy) {
     *out = GpuBvh8();
     if (ntri == 0) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
@@ -670,9 +670,7 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
     hipLaunchKernelGGL(leaf_ones_kernel, dim3(blocks(ntri)), dim3(kBlock), 0, s, ntris, ntri);  // 1 tri per leaf
     GB_TRY(hipGetLastError());
 
-    // PLOC iterations (search radius: env SPT_PLOC_RADIUS = 8, 16, 32 or 64)
-    const char* rv = std::getenv("SPT_PLOC_RADIUS");
-    const int radius = rv ? std::atoi(rv) : kDefaultRadius;
+    // PLOC iterations (search radius 8, 16, 32 or 64: spt_config.ploc_radius)
     size_t scan_bytes = 0;
     GB_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, flags, scan, (int)ntri, s));
     void* scan_ws = nullptr;
@@ -715,11 +713,10 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
     out->bvh2_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     out->ploc_iterations = iters;
 
-    // SAH-optimal collapse decisions, bottom-up by merge iteration (env
-    // SPT_GPU_COLLAPSE=greedy keeps the greedy collapse)
+    // SAH-optimal collapse decisions, bottom-up by merge iteration
+    // (spt_config.collapse = 1 keeps the greedy collapse)
     DpNode* dp = nullptr;
-    const char* gc = std::getenv("SPT_GPU_COLLAPSE");
-    if (!(gc && std::strcmp(gc, "greedy") == 0) && ntri > 1) {
+    if (!greedy && ntri > 1) {
         GB_TRY(tmp.get(&dp, ntri - 1));
         for (const auto& m : made)
             hipLaunchKernelGGL(dp_kernel, dim3(blocks(m.second)), dim3(kBlock), 0, s, lo, hi, kids2, ntris, ntri,

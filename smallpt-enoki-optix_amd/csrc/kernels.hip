@@ -1033,35 +1033,36 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
     if (!m || id < 0) return;                                    // active = neq(tri_id,-1) && mask
     const int32_t slot = a.sc.orig2slot[id];
     const float t = a.t[i], u = a.u[i], v = a.v[i];
-    if (a.px) {
-        a.px[i] = a.ox[i] + t * a.dx[i];
-        a.py[i] = a.oy[i] + t * a.dy[i];
-        a.pz[i] = a.oz[i] + t * a.dz[i];
-    }
-    if (a.gnx) {
+    // every output plane may be NULL on its own (spt.h spt_hit_info)
+    if (a.px) a.px[i] = a.ox[i] + t * a.dx[i];
+    if (a.py) a.py[i] = a.oy[i] + t * a.dy[i];
+    if (a.pz) a.pz[i] = a.oz[i] + t * a.dz[i];
+    if (a.gnx || a.gny || a.gnz) {
         const float4 p0 = a.sc.tris[(size_t)slot * 3], p1 = a.sc.tris[(size_t)slot * 3 + 1],
                      p2 = a.sc.tris[(size_t)slot * 3 + 2];
         const V3 g = normalize(cross(v3(p1.x - p0.x, p1.y - p0.y, p1.z - p0.z),  // add_math.h:9-16
                                      v3(p2.x - p0.x, p2.y - p0.y, p2.z - p0.z)));
-        a.gnx[i] = g.x; a.gny[i] = g.y; a.gnz[i] = g.z;
+        if (a.gnx) a.gnx[i] = g.x;
+        if (a.gny) a.gny[i] = g.y;
+        if (a.gnz) a.gnz[i] = g.z;
     }
     const float w = (1.0f - u) - v;
     const float4 m0 = a.sc.snrm[(size_t)slot * 3];
-    if (a.snx) {
+    if (a.snx || a.sny || a.snz) {
         const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1], m2 = a.sc.snrm[(size_t)slot * 3 + 2];
-        a.snx[i] = (w * m0.x + u * m1.x) + v * m2.x;
-        a.sny[i] = (w * m0.y + u * m1.y) + v * m2.y;
-        a.snz[i] = (w * m0.z + u * m1.z) + v * m2.z;
+        if (a.snx) a.snx[i] = (w * m0.x + u * m1.x) + v * m2.x;
+        if (a.sny) a.sny[i] = (w * m0.y + u * m1.y) + v * m2.y;
+        if (a.snz) a.snz[i] = (w * m0.z + u * m1.z) + v * m2.z;
     }
-    if (a.tcu) {
+    if (a.tcu || a.tcv) {
         float cu = 0.0f, cv = 0.0f;
         if (a.sc.tc) {
             const float* c = a.sc.tc + (size_t)slot * 6;
             cu = (w * c[0] + u * c[2]) + v * c[4];
             cv = (w * c[1] + u * c[3]) + v * c[5];
         }
-        a.tcu[i] = cu;
-        a.tcv[i] = cv;
+        if (a.tcu) a.tcu[i] = cu;
+        if (a.tcv) a.tcv[i] = cv;
     }
     if (a.mat_id) a.mat_id[i] = (int32_t)f2u(m0.w);
 }
@@ -1117,9 +1118,7 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     // one lane per ray by default: the reference's first bounce (camera rays)
     // traces 25-30 % faster in lockstep waves; the persistent kernel wins on
     // incoherent rays (+25-36 %) — tools/isect_api_bench.py, DESIGN.md §4
-    const char* pe = getenv("SPT_PUBLIC_PERSISTENT");  // read per call (tests switch it)
-    const bool persistent = pe && atoi(pe) != 0;
-    if (a.sc.nodes8 && persistent) {
+    if (a.sc.nodes8 && a.persistent) {
         static thread_local size_t cached_lds = 0;
         static thread_local uint32_t cached = 0;
         static thread_local int cached_dev = -1;

@@ -74,6 +74,7 @@ struct IsectPublicArgs {
     uint32_t n;
     int32_t closest;
     uint32_t refill_idle;  // persistent BVH8 kernel: refill a wave once this many lanes are idle
+    uint32_t persistent;   // 1: the persistent lane-refill kernel (spt_config.public_persistent)
 };
 
 // Blocks are dealt round-robin over the 8 XCDs (block b and b + 8 share one

@@ -31,7 +31,9 @@ EXPORTED = [
     "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
     "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write", "spt_pbrt_load",
+    "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
 ]
+SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
 
 
 class SptError(RuntimeError):
@@ -95,6 +97,21 @@ class SceneStats(ctypes.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class Config(ctypes.Structure):
+    """spt_config (include/spt.h): the library's build and tuning knobs."""
+    _fields_ = [("build", c_uint32), ("bvh_width", c_uint32), ("gpu_build_min_tris", c_uint64),
+                ("collapse", c_uint32), ("ploc_radius", c_uint32), ("stack_slack", c_uint32),
+                ("pipeline", c_uint32), ("fused_max_paths", c_uint64), ("wavefront_paths", c_uint32),
+                ("streams", c_uint32), ("isect_refill_idle", c_uint32), ("isect_static_share_q8", c_uint32),
+                ("isect_chunk", c_uint32), ("isect_grid_q8", c_uint32), ("xcd_remap", c_uint32),
+                ("fused_refill_idle", c_uint32), ("fused_static_share_q8", c_uint32), ("fused_grid_q8", c_uint32),
+                ("plane_pad", c_uint32), ("film_budget_bytes", c_uint64),
+                ("public_persistent", c_uint32), ("public_refill_idle", c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 class Mesh(ctypes.Structure):
     _fields_ = [("pos_tri", POINTER(c_int32)), ("pos", POINTER(c_float)), ("nvert", c_uint64), ("ntri", c_uint64),
                 ("nrm_tri", POINTER(c_int32)), ("nrm", POINTER(c_float)), ("nnrm", c_uint64),
@@ -139,6 +156,10 @@ def _load() -> ctypes.CDLL:
         "spt_mesh_free": (None, [POINTER(Mesh)]),
         "spt_pbrt_load": (i32, [c_char_p, POINTER(Mesh), POINTER(PbrtInfo)]),
         "spt_pfm_write": (i32, [c_char_p, vp, vp, vp, u32, u32]),
+        "spt_default_config": (None, [POINTER(Config)]),
+        "spt_scene_create_cfg": (i32, [vp, vp, u64, u64, vp, vp, u64, vp, vp, u64, vp, POINTER(Config), POINTER(vp)]),
+        "spt_scene_set_config": (i32, [vp, POINTER(Config)]),
+        "spt_scene_get_config": (i32, [vp, POINTER(Config)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -161,6 +182,56 @@ def default_params() -> RenderParams:
     return p
 
 
+def default_config() -> Config:
+    c = Config()
+    lib.spt_default_config(ctypes.byref(c))
+    return c
+
+
+# SPT_* environment overrides of spt_config (the host's knobs; the library
+# itself reads no environment): variable -> (field, parser)
+_ENV_CONFIG = {
+    "SPT_BUILD": ("build", lambda v: {"auto": 0, "host": 1, "gpu": 2}[v]),
+    "SPT_BVH": ("bvh_width", int),
+    "SPT_GPU_BUILD_MIN_TRIS": ("gpu_build_min_tris", int),
+    "SPT_COLLAPSE": ("collapse", lambda v: {"sah": 0, "dp": 0, "greedy": 1}[v]),
+    "SPT_PLOC_RADIUS": ("ploc_radius", int),
+    "SPT_STACK_SLACK": ("stack_slack", int),
+    "SPT_FUSED": ("pipeline", lambda v: {"0": 1, "1": 2, "2": 0, "auto": 0}[v]),
+    "SPT_FUSED_MAX_PATHS": ("fused_max_paths", int),
+    "SPT_WAVEFRONT_PATHS": ("wavefront_paths", int),
+    "SPT_STREAMS": ("streams", int),
+    "SPT_REFILL_IDLE": ("isect_refill_idle", int),
+    "SPT_STATIC_SHARE_Q8": ("isect_static_share_q8", int),
+    "SPT_CHUNK": ("isect_chunk", int),
+    "SPT_ISECT_GRID_Q8": ("isect_grid_q8", int),
+    "SPT_XCD": ("xcd_remap", int),
+    "SPT_FUSED_IDLE": ("fused_refill_idle", int),
+    "SPT_FUSED_STATIC_SHARE_Q8": ("fused_static_share_q8", int),
+    "SPT_FUSED_GRID_Q8": ("fused_grid_q8", int),
+    "SPT_PLANE_PAD": ("plane_pad", int),
+    "SPT_FILM_BUDGET": ("film_budget_bytes", int),
+    "SPT_PUBLIC_PERSISTENT": ("public_persistent", int),
+    "SPT_PUBLIC_REFILL_IDLE": ("public_refill_idle", int),
+}
+
+
+def config_from_env(base: Config = None, environ=None) -> Config:
+    """spt_config with the SPT_* environment variables applied over `base`
+    (default: spt_default_config).  An unparsable value raises ValueError."""
+    env = os.environ if environ is None else environ
+    c = default_config() if base is None else Config.from_buffer_copy(base)
+    for var, (field, parse) in _ENV_CONFIG.items():
+        v = env.get(var)
+        if v is None or v == "":
+            continue
+        try:
+            setattr(c, field, parse(v.strip()))
+        except (KeyError, ValueError) as e:
+            raise ValueError(f"{var}={v!r}: not a valid spt_config.{field}") from e
+    return c
+
+
 def tile_rows(height: int, tile_index: int, tile_count: int, rows_per_group: int):
     import numpy as np
     n = lib.spt_tile_rows(height, tile_index, tile_count, rows_per_group, None, 0)
@@ -171,6 +242,7 @@ def tile_rows(height: int, tile_index: int, tile_count: int, rows_per_group: int
 
 __all__ = [
     "lib", "check", "SptError", "Rays", "Hits", "HitInfo", "Camera", "RenderParams", "RenderStats",
-    "SceneStats", "Mesh", "default_params", "tile_rows", "EXPORTED", "LIB_PATH", "REPO_ROOT",
+    "SceneStats", "Mesh", "Config", "default_params", "default_config", "config_from_env", "tile_rows", "EXPORTED",
+    "LIB_PATH", "REPO_ROOT",
     "PCG32_DEFAULT_STATE", "SPT_RNG_Y_FIRST", "SPT_RNG_X_FIRST", "SPT_FLAG_TIMING", "c_uint8",
 ]

@@ -21,7 +21,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import Hits, HitInfo, Rays, RenderParams, RenderStats, SceneStats, check, lib
+from ._lib import Config, Hits, HitInfo, Rays, RenderParams, RenderStats, SceneStats, check, config_from_env, lib
 
 RAY_TMIN = 0.001  # ray.h:16
 RAY_TMAX = 1e20
@@ -84,10 +84,14 @@ class TriangleHitInfo:
 class HipBackend:
     """OptixBackend replacement: init / set_triangles_soup / intersect."""
 
-    def __init__(self):
+    def __init__(self, config: Optional[Config] = None):
         self._scene = ctypes.c_void_p()
         self.device = None
         self.stats: dict = {}
+        # spt_config: explicit base (default: the library's), with the SPT_*
+        # environment variables applied over it before every call that reads it
+        self.base_config = config
+        self._applied = None
 
     def __del__(self):
         if getattr(self, "_scene", None) and self._scene.value:
@@ -119,11 +123,15 @@ class HipBackend:
         if self._scene.value:
             lib.spt_scene_destroy(self._scene)
             self._scene = ctypes.c_void_p()
-        check(lib.spt_scene_create_ex(
+        cfg = config_from_env(self.base_config)
+        if build:
+            cfg.build = build
+        check(lib.spt_scene_create_cfg(
             _host_ptr(pt), _host_ptr(pos), pos.size // 3, ntri,
             _host_ptr(nt), _host_ptr(nrm), 0 if nrm is None else nrm.size // 3,
             _host_ptr(tt), _host_ptr(tc), 0 if tc is None else tc.size // 2,
-            _host_ptr(mat), build, ctypes.byref(self._scene)), "spt_scene_create")
+            _host_ptr(mat), ctypes.byref(cfg), ctypes.byref(self._scene)), "spt_scene_create")
+        self._applied = bytes(cfg)
         st = SceneStats()
         check(lib.spt_scene_get_stats(self._scene, ctypes.byref(st)), "spt_scene_get_stats")
         self.stats = st.as_dict()
@@ -140,6 +148,30 @@ class HipBackend:
     def handle(self):
         return self._scene
 
+    def sync_config(self) -> None:
+        """Apply base config + SPT_* environment overrides if they changed."""
+        cfg = config_from_env(self.base_config)
+        if bytes(cfg) != self._applied:
+            check(lib.spt_scene_set_config(self._scene, ctypes.byref(cfg)), "spt_scene_set_config")
+            self._applied = bytes(cfg)
+
+    @property
+    def config(self) -> dict:
+        c = Config()
+        check(lib.spt_scene_get_config(self._scene, ctypes.byref(c)), "spt_scene_get_config")
+        return c.as_dict()
+
+    def _dev_mask(self, mask, dev, stream):
+        """Device uint8 copy of mask, kept alive until the launch's stream has
+        consumed it (record_stream: the caching allocator will not hand the
+        block to another stream's allocation before that)."""
+        if mask is None:
+            return None, 0, None
+        m = torch.as_tensor(mask, dtype=torch.uint8).to(dev).contiguous().reshape(-1)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        m.record_stream(s)
+        return m.data_ptr(), m.numel(), m
+
     def intersect_raw(self, rays: Ray3, mask=None, do_closest: bool = True, stream=None,
                       out: Optional[Sequence[torch.Tensor]] = None):
         """__raygen__rg semantics (wavefront_isect.cu:80-112).  Returns
@@ -153,15 +185,12 @@ class HipBackend:
             v = torch.zeros(n, dtype=torch.float32, device=dev)
         else:
             tri_id, t, u, v = out
-        mask_ptr, mask_size = None, 0
-        if mask is not None:
-            m = torch.as_tensor(mask, dtype=torch.uint8).to(dev).contiguous().reshape(-1)
-            mask_ptr, mask_size = m.data_ptr(), m.numel()
+        self.sync_config()
+        mask_ptr, mask_size, m = self._dev_mask(mask, dev, stream)
         hits = Hits(tri_id.data_ptr(), t.data_ptr(), u.data_ptr(), v.data_ptr())
         rs = rays.c_struct()
         check(lib.spt_intersect(self._scene, ctypes.byref(rs), mask_ptr, mask_size, ctypes.byref(hits), n,
                                 1 if do_closest else 0, _stream_handle(stream)), "spt_intersect")
-        self._keep = mask  # keep the mask alive until the stream is synchronised by the caller
         return tri_id, t, u, v
 
     # optix_backend.h:422-487
@@ -176,10 +205,7 @@ class HipBackend:
                        gn[0].data_ptr(), gn[1].data_ptr(), gn[2].data_ptr(),
                        sn[0].data_ptr(), sn[1].data_ptr(), sn[2].data_ptr(),
                        tc[0].data_ptr(), tc[1].data_ptr(), mat.data_ptr())
-        mask_ptr, mask_size = None, 0
-        if mask is not None:
-            m = torch.as_tensor(mask, dtype=torch.uint8).to(dev).contiguous().reshape(-1)
-            mask_ptr, mask_size = m.data_ptr(), m.numel()
+        mask_ptr, mask_size, m = self._dev_mask(mask, dev, stream)
         rs = rays.c_struct()
         hits = Hits(tri_id.data_ptr(), t.data_ptr(), u.data_ptr(), v.data_ptr())
         check(lib.spt_hit_info_compute(self._scene, ctypes.byref(rs), ctypes.byref(hits), mask_ptr, mask_size, n,
@@ -235,8 +261,8 @@ def make_params(width: int, height: int, spp: int, max_depth: int, camera: Optio
 class Scene:
     """main.cpp:286-352: add_triangle_mesh / commit / intersect, plus render()."""
 
-    def __init__(self):
-        self.backend = HipBackend()
+    def __init__(self, config: Optional[Config] = None):
+        self.backend = HipBackend(config)
         self.mesh = None
         self.pbrt_info: Optional[dict] = None
 
@@ -274,6 +300,7 @@ class Scene:
             film = torch.empty((3, rows, params.width), dtype=torch.float32, device=self.backend.device)
         assert film.is_contiguous() and film.numel() >= 3 * rows * params.width
         st = RenderStats()
+        self.backend.sync_config()
         check(lib.spt_render(self.backend.handle, ctypes.byref(params), film.data_ptr(), ctypes.byref(st),
                              _stream_handle(stream)), "spt_render")
         return film, st.as_dict()

@@ -134,7 +134,8 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     structs = {"spt_render_params": _lib.RenderParams, "spt_render_stats": _lib.RenderStats,
                "spt_scene_stats": _lib.SceneStats, "spt_rays": _lib.Rays, "spt_hits": _lib.Hits,
-               "spt_hit_info": _lib.HitInfo, "spt_camera": _lib.Camera, "spt_mesh": _lib.Mesh}
+               "spt_hit_info": _lib.HitInfo, "spt_camera": _lib.Camera, "spt_mesh": _lib.Mesh,
+               "spt_config": _lib.Config}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, ct in structs.items():
         lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
@@ -151,3 +152,43 @@ def test_struct_layouts_match_header(tmp_path):
         ct = structs[cname]
         got = ctypes.sizeof(ct) if field == "sizeof" else getattr(ct, field).offset
         assert got == int(val), (cname, field, got, val)
+
+
+def test_config_defaults_and_env_overrides():
+    """spt_config carries every knob (the library reads no environment);
+    the Python host maps SPT_* variables onto it as overrides."""
+    c = sptamd.default_config()
+    assert (c.build, c.bvh_width, c.collapse, c.ploc_radius) == (0, 8, 0, 16)
+    assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
+    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 24      # spt.h docs = code
+    assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
+    e = sptamd.config_from_env(environ={"SPT_STREAMS": "2", "SPT_BUILD": "gpu", "SPT_FUSED": "0",
+                                        "SPT_FILM_BUDGET": "1000", "SPT_COLLAPSE": "greedy", "SPT_BVH": "2"})
+    assert (e.streams, e.build, e.pipeline, e.film_budget_bytes, e.collapse, e.bvh_width) == (2, 2, 1, 1000, 1, 2)
+    with pytest.raises(ValueError):
+        sptamd.config_from_env(environ={"SPT_BUILD": "cuda"})
+
+
+@pytest.mark.parametrize("field,value", [("streams", 0), ("streams", 5), ("bvh_width", 4), ("ploc_radius", 12),
+                                         ("isect_refill_idle", 65), ("film_budget_bytes", 0), ("pipeline", 3)])
+def test_config_validation_without_gpu(field, value):
+    c = sptamd.default_config()
+    setattr(c, field, value)
+    pt = np.array([0, 1, 2], np.int32)
+    pos = np.zeros(9, np.float32)
+    out = ctypes.c_void_p()
+    st = _lib.lib.spt_scene_create_cfg(pt.ctypes.data, pos.ctypes.data, 3, 1, None, None, 0, None, None, 0, None,
+                                       ctypes.byref(c), ctypes.byref(out))
+    assert st == 1 and field.encode() in _lib.lib.spt_last_error()
+    assert _lib.lib.spt_scene_set_config(None, ctypes.byref(c)) == 1
+
+
+def test_library_reads_no_environment():
+    """the tuning knobs are C ABI fields, not getenv.
+    (The .so still imports getenv: rocPRIM's headers, behind hipcub, read
+    their own debug variables; no source of ours does.)"""
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "smallpt-enoki-optix_amd", "csrc", "*"))
+    assert len(srcs) > 10
+    for f in srcs:
+        assert not re.search(r"\b(getenv|secure_getenv)\s*\(", open(f).read()), f
