@@ -4,7 +4,8 @@ Workload (BASELINE.json configs[1]): mitsuba_synth (stand-in for the absent
 mitsuba.obj), 1024 x 1024, 64 spp, 8 ray casts per path.  One step = one
 full render of that image: every rank renders its interleaved row-group
 tile, the fp32 tiles are gathered to rank 0 over RCCL and assembled.  With N
-GPUs the same image is split N ways (strong scaling).
+GPUs the same image is split N ways (strong scaling).  --config 0..4 selects
+BASELINE.json configs[i] (0 = the 256^2 x 4 spp plumbing run).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -27,12 +28,14 @@ sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_JSON = os.path.join(ROOT, "profiles", "isect_pmc.json")  # tools/pmc_isect.sh output
 VALU_PEAK_G = 256 * 4 * 2.4 / 2  # wave64 VALU instr/s (G): 1024 SIMDs, 2 cycles each at 2.4 GHz (MI355X_MICROARCH.md)
-ISECT_BYTES_PER_CAST = 44      # ray 24 B + meta 4 B in, hit 16 B out
+ISECT_BYTES_PER_CAST = 52      # queue idx 4 + ray 32 (o, d, tmin, tmax) in, hit 16 out
+KERNEL_BYTES_PER_CAST = 44     # what isect_queue_kernel moves: ray 24 + meta 4 in, hit 16 out
 FUSED_BYTES_PER_PATH = 12      # per-sample film RGB write
 
 
 # BASELINE.json configs (index = position in "configs"); 1 is the headline.
 CONFIGS = {
+    0: dict(scene="mitsuba_synth", width=256, height=256, spp=4, depth=4, smallpt=False),
     1: dict(scene="mitsuba_synth", width=1024, height=1024, spp=64, depth=8, smallpt=False),
     2: dict(scene="cornell_spheres", width=1024, height=1024, spp=1024, depth=10, smallpt=True),
     3: dict(scene="mitsuba_synth", width=4096, height=4096, spp=256, depth=8, smallpt=False),
@@ -46,7 +49,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
-                    help="BASELINE.json configs[i]: 1 mitsuba 1024^2x64 (headline), 2 Cornell 1024^2x1024 "
+                    help="BASELINE.json configs[i]: 0 mitsuba 256^2x4 depth 4 (plumbing), 1 mitsuba 1024^2x64 "
+                         "(headline), 2 Cornell 1024^2x1024 "
                          "(emitters, albedo, roulette), 3 mitsuba 4096^2x256, 4 10M-tri city 1920x1080x64")
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
@@ -62,7 +66,8 @@ def parse():
     ap.add_argument("--timing-all", action="store_true",
                     help="HIP events around every launch (shade/refill/resolve ms too; costs ~5%% host time)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = the CPUs this process may use: affinity mask and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--save", default="", help="write the rank-0 image (.npy) here")
     args = ap.parse_args()
@@ -98,6 +103,31 @@ def _cpu_model():
     return None
 
 
+def cpu_share():
+    """CPUs this process may run on: the affinity mask, bounded by a cgroup
+    CPU quota when one is set (cpu.max), and where each figure came from."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return n, {"affinity_cpus": aff, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count()}
+
+
 def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
     """Measured HBM peak for the roofline (BASELINE.md plan): a device-to-device
     copy of nbytes, read + write bytes over the best of reps (HIP events)."""
@@ -119,12 +149,16 @@ def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
 
 
 def cpu_baseline(mesh, args, threads, kw, albedo, emission):
-    """Oracle (oracle/, a C restatement of main.cpp:354-446) on a bounded row
-    sample of the same workload, on this host's cores."""
+    """Oracle (oracle/, a C restatement of main.cpp:354-446, binned-SAH BVH2,
+    one pthread per CPU this process may use) on a bounded row sample of the
+    same workload, on this host's cores."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
 
+    share, share_src = cpu_share()
+    if not threads:
+        threads = share
     sc = O.OracleScene(mesh, albedo=albedo, emission=emission)
     p = O.reference_params(args.width, args.height, args.spp, args.depth, **kw)
     # calibrate on 8 rows spread over the image (sky rows at the top are cheap)
@@ -140,10 +174,10 @@ def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     dt = time.perf_counter() - t0
     paths = rows.size * args.width * args.spp
     return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "cpu": _cpu_model(), "host_cpus": os.cpu_count(),
+            "cpu": _cpu_model(), "cpus": share_src,
             "sample": f"{rows.size} of {args.height} rows (evenly spaced) x {args.width} px x {args.spp} spp, "
                       f"depth {args.depth}: {paths} paths, {casts} casts in {dt:.2f} s "
-                      f"(oracle: C restatement, median-split BVH, {threads} threads)"}
+                      f"(oracle: C restatement, binned-SAH BVH2, {threads} threads)"}
 
 
 def main():
@@ -212,9 +246,17 @@ def main():
     film = tg.tile_view()
     stream = torch.cuda.current_stream()
 
-    def step():
+    gather_ev = []
+
+    def step(timed=False):
         _, st = scene.render(params, film=film, stream=stream)
+        if timed:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
         tg.gather()
+        if timed:
+            e1.record(stream)
+            gather_ev.append((e0, e1))
         return st
 
     for _ in range(args.warmup):
@@ -228,7 +270,7 @@ def main():
            "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0}
     st = {}
     for _ in range(args.steps):
-        st = step()
+        st = step(timed=True)
         for k in agg:
             agg[k] += st[k]
     torch.cuda.synchronize()
@@ -251,29 +293,30 @@ def main():
 
     paths = W * H * args.spp * args.steps
     value = paths / elapsed / 1e6
+    gather_ms = sum(e0.elapsed_time(e1) for e0, e1 in gather_ev) / max(1, len(gather_ev))
     if rank == 0:
-        # roofline of the dominant kernel: algorithmic bytes per launch / average
-        # launch duration (HIP events on each launch's own stream, rank 0's
-        # tile; the figure rocprofv3's per-kernel average reproduces).
-        # Wavefront: isect_queue_kernel, 44 B per ray cast.  Fused:
+        # Roofline of the dominant kernel.  Wavefront:
+        # isect_queue_kernel, SURVEY §8(d)'s 52 B per ray cast.  The K
+        # sub-wavefront streams' isect launches overlap, so the headline
+        # divides the bytes of ALL isect launches by the union of their
+        # intervals (HIP events on each launch's own stream): the time the
+        # kernel occupies the chip, <= ms_per_step.  `per_launch` keeps the
+        # per-launch figure (a 1/K-chip rate when K > 1).  Fused:
         # render_fused_kernel, whose only HBM stream is the per-sample film
-        # write (12 B per path; rays stay in registers).  The wavefront runs K
-        # sub-wavefronts on K streams, so isect launches overlap: `chip_busy`
-        # divides the bytes of all launches by the union of their intervals
-        # (the time the isect kernel occupies the chip).  `valu` is the VALU
-        # issue rate over that busy time from the committed PMC pass, against
-        # the chip's wave64 VALU issue peak: traversal is issue- and
-        # latency-bound, not HBM-bound.
+        # write (12 B per path; rays stay in registers).
         fused = bool(st.get("fused"))
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
+        casts_per_launch = agg["ray_casts"] / launches
         if fused:
+            bytes_per_unit, kernel_bytes_per_unit = FUSED_BYTES_PER_PATH, FUSED_BYTES_PER_PATH
             total_bytes = st["paths"] * args.steps * FUSED_BYTES_PER_PATH
         else:
+            bytes_per_unit, kernel_bytes_per_unit = ISECT_BYTES_PER_CAST, KERNEL_BYTES_PER_CAST
             total_bytes = agg["ray_casts"] * ISECT_BYTES_PER_CAST
         bytes_per_launch = total_bytes / launches
         busy_ms = agg["isect_busy_ms"]
-        achieved_busy = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+        achieved = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
         per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         # whole-path bytes: B_path = 84 + 120 S + 60 C, S = casts and
         # C = continuations per path, over the whole frame time, against the spec
@@ -284,13 +327,16 @@ def main():
         path_gbs = b_path * paths / elapsed / 1e9
         copy_gbs = stream_copy_gbs(torch, dev)
         pmc = None
-        if args.config == 1 and not fused and world == 1 and os.path.exists(PMC_JSON):  # PMC passes (profiles/)
-            pmc = json.load(open(PMC_JSON))
-        traffic = round(pmc["traffic_bytes_per_launch"]) if pmc and "traffic_bytes_per_launch" in pmc else None
+        if os.path.exists(PMC_JSON) and not fused and world == 1:  # PMC passes (profiles/, tools/pmc_isect.py)
+            pmc = json.load(open(PMC_JSON)).get(f"config{args.config}")
+        traffic = traffic_per_cast = None
+        if pmc and pmc.get("traffic_bytes_per_cast"):
+            traffic_per_cast = pmc["traffic_bytes_per_cast"]
+            traffic = round(traffic_per_cast * casts_per_launch)
         valu = None
-        if pmc and "valu_insts_per_launch" in pmc and busy_ms > 0:
-            rate = pmc["valu_insts_per_launch"] * launches / (busy_ms * 1e-3) / 1e9
-            valu = {"insts_per_launch": round(pmc["valu_insts_per_launch"]), "achieved": round(rate, 1),
+        if pmc and pmc.get("valu_insts_per_cast") and busy_ms > 0:
+            rate = pmc["valu_insts_per_cast"] * agg["ray_casts"] / (busy_ms * 1e-3) / 1e9
+            valu = {"insts_per_cast": round(pmc["valu_insts_per_cast"], 2), "achieved": round(rate, 1),
                     "peak": VALU_PEAK_G, "unit": "G wave64 VALU instr/s over isect busy time",
                     "frac": round(rate / VALU_PEAK_G, 4)}
         rec = {
@@ -307,30 +353,37 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
+            "pipeline_rule": "auto: fused for tiles of <= 16M paths, else wavefront (DESIGN.md §6)"
+                             if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
                        "workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
                        "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4)},
-            "roofline": {"bound": "hbm", "achieved": round(per_launch, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(per_launch / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",
+                         "basis": "algorithmic bytes of all launches / union of their intervals (isect busy)",
+                         "bytes_per_unit": bytes_per_unit, "kernel_bytes_per_unit": kernel_bytes_per_unit,
+                         "unit_of_work": "path" if fused else "ray cast",
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                         "avg_launch_ms": round(avg_ms, 4),
+                         "traffic_per_unit": traffic_per_cast,
+                         "traffic_ratio": round(traffic / bytes_per_launch, 3) if traffic else None,
+                         "busy_ms_per_step": round(busy_ms / args.steps, 4),
                          "launches_per_step": round(launches / args.steps, 2),
-                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) if pmc else None,
-                         "chip_busy": {"busy_ms_per_step": round(busy_ms / args.steps, 4),
-                                       "achieved": round(achieved_busy, 2),
-                                       "frac": round(achieved_busy / HBM_PEAK_GBS, 5),
-                                       "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4)
-                                       if busy_ms else None},
+                         "avg_launch_ms": round(avg_ms, 4),
+                         "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None,
+                         "per_launch": {"achieved": round(per_launch, 2), "frac": round(per_launch / HBM_PEAK_GBS, 5),
+                                        "note": f"per-launch duration; {st.get('streams')} streams overlap"},
+                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) + f"#config{args.config}" if pmc else None,
                          "valu": valu,
                          "stream_copy_peak": round(copy_gbs, 1),
                          "path": {"bytes_per_path": round(b_path, 1),
                                   "formula": "84 + 120*S + 60*C (SURVEY 8d), S=%.4f C=%.4f" % (s_bar, c_bar),
                                   "achieved": round(path_gbs, 1), "frac": round(path_gbs / HBM_PEAK_GBS, 4),
                                   "frac_of_stream_copy": round(path_gbs / copy_gbs, 4)}},
+            "gather_ms": round(gather_ms, 4),
             "kernel_ms_per_step": {k: round(agg[k] / args.steps, 3) for k in
                                    (("isect_ms", "shade_ms", "camera_ms", "resolve_ms") if args.timing_all
                                     else ("isect_ms",))},

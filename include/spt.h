@@ -242,6 +242,14 @@ spt_status spt_scene_set_albedo(spt_scene scene, const float* albedo_rgb, uint32
 spt_status spt_scene_set_emission(spt_scene scene, const float* emission_rgb, uint32_t nmat);
 
 spt_status spt_scene_get_stats(spt_scene scene, spt_scene_stats* out);
+
+/* The host builders alone, without a device (diagnostics; the host sanitizer
+ * run drives the builders through it): triangle soup tri_verts (ntri x 9
+ * floats: v0 v1 v2), cfg->bvh_width 2 or 8 and cfg->collapse (NULL =
+ * defaults).  Fills ntri, nodes, leaves, max_depth, max_leaf, bvh_width,
+ * builder (SPT_BUILD_HOST_SAH), build_ms and sah_cost; device_bytes = 0. */
+spt_status spt_bvh_build_stats(const float* tri_verts, uint64_t ntri, const spt_config* cfg,
+                               spt_scene_stats* out);
 spt_status spt_scene_destroy(spt_scene scene);
 
 /* OptixBackend::intersect (optix_backend.h:422-460) → __raygen__rg

@@ -19,6 +19,19 @@
  *     (add_math.h:3-7).  Parity vs OptiX unpinned (OptiX absent).
  * Floating-point: compiled with -ffp-contract=off; every fused multiply-add
  * is an explicit fmaf().
+ *
+ * Arithmetic variants (compile-time, oracle/Makefile builds each as its own
+ * liboracle_alt_*.so): the choices the reference leaves to code we cannot
+ * run, each swapped for a plausible alternative so the tests can bound how
+ * much the image depends on it (tests/test_parity_tolerance.py):
+ *   ORACLE_ALT_SINCOS     libm sinf/cosf instead of Cephes (Enoki sincos, mapping.h:9,25)
+ *   ORACLE_ALT_RSQRT      normalize with a 1-ulp-high reciprocal square root
+ *                         (Enoki normalize = v * rsqrt(|v|^2), CUDA rsqrt.approx)
+ *   (fp-contract)         -ffp-contract=fast -mfma: products fused into FMAs
+ *                         wherever the compiler likes (nvcc's default contraction)
+ *   ORACLE_ALT_TRI        Moller-Trumbore (not watertight) instead of the Woop
+ *                         test standing in for OptiX's triangle test (optix_backend.h:314)
+ *   (all)                 the four together
  */
 #include "oracle.h"
 
@@ -69,6 +82,11 @@ void oracle_pcg32_floats(uint64_t initstate, uint64_t initseq, float* out, int32
 /* Cephes single-precision joint sin/cos as used by Enoki's sincos (called at
  * mapping.h:9 and mapping.h:25). */
 void oracle_sincos(float x, float* s_out, float* c_out) {
+#ifdef ORACLE_ALT_SINCOS
+    *s_out = sinf(x);
+    *c_out = cosf(x);
+    return;
+#endif
     float xa = fabsf(x);
     int32_t j = (int32_t)(xa * 1.2732395447351626862f);
     j = (j + 1) & ~1;
@@ -99,6 +117,9 @@ static inline v3 cross3(v3 a, v3 b) {
 /* Enoki normalize: v * rsqrt(squared_norm(v)); restated as v * (1/sqrt). */
 static inline v3 normalize3(v3 v) {
     float inv = 1.0f / sqrtf(dot3(v, v));
+#ifdef ORACLE_ALT_RSQRT
+    inv = nextafterf(inv, INFINITY);
+#endif
     return mk(v.x * inv, v.y * inv, v.z * inv);
 }
 static inline float get(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z); }
@@ -252,8 +273,20 @@ static int cmp_prim(const void* a, const void* b) {
     return (*(const int32_t*)a < *(const int32_t*)b) ? -1 : 1;
 }
 
-/* Median-split BVH (independent of the product's binned-SAH BVH). */
-static void build_node(oscene* s, float* cen, int64_t ni, int64_t first, int64_t count) {
+/* Binned-SAH BVH2 (16 bins per axis over the centroid bounds; leaves of at
+ * most 4 triangles unless splitting does not pay; a degenerate centroid
+ * spread, or depth 48, falls back to a median split, so the tree is at most
+ * 48 + log2(n) deep).  Independent of the product's
+ * builders (bvh_build.cpp, gpu_build.hip); the closest hit does not depend on
+ * the tree (ties go to the smaller id), which tests/test_oracle.py checks
+ * against brute force. */
+#define SAH_BINS 16
+static float half_area(const float* lo, const float* hi) {
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (!(dx >= 0.0f)) return 0.0f;
+    return dx * dy + dy * dz + dz * dx;
+}
+static void build_node(oscene* s, float* cen, int64_t ni, int64_t first, int64_t count, int depth) {
     onode* nd = &s->nodes[ni];
     for (int k = 0; k < 3; k++) { nd->bmin[k] = INFINITY; nd->bmax[k] = -INFINITY; }
     float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -271,20 +304,90 @@ static void build_node(oscene* s, float* cen, int64_t ni, int64_t first, int64_t
             if (c > cmax[k]) cmax[k] = c;
         }
     }
-    if (count <= 4) { nd->left = (int32_t)first; nd->count = (int32_t)count; return; }
-    int axis = 0;
-    float ext[3] = {cmax[0] - cmin[0], cmax[1] - cmin[1], cmax[2] - cmin[2]};
-    if (ext[1] > ext[axis]) axis = 1;
-    if (ext[2] > ext[axis]) axis = 2;
-    g_sort.cen = cen; g_sort.axis = axis;
-    qsort(&s->prims[first], (size_t)count, sizeof(int32_t), cmp_prim);
-    int64_t half = count / 2;
+    if (count <= 2) { nd->left = (int32_t)first; nd->count = (int32_t)count; return; }
+    /* SAH over binned centroids: cost = A_l * n_l + A_r * n_r (traversal cost 1 per node area) */
+    int best_axis = -1, best_split = 0;
+    float best_cost = INFINITY;
+    for (int axis = 0; axis < 3; axis++) {
+        float ext = cmax[axis] - cmin[axis];
+        if (!(ext > 0.0f)) continue;
+        float lo[SAH_BINS][3], hi[SAH_BINS][3];
+        int64_t cnt[SAH_BINS];
+        for (int b = 0; b < SAH_BINS; b++) {
+            cnt[b] = 0;
+            for (int k = 0; k < 3; k++) { lo[b][k] = INFINITY; hi[b][k] = -INFINITY; }
+        }
+        float scale = (float)SAH_BINS / ext;
+        for (int64_t i = first; i < first + count; i++) {
+            int32_t p = s->prims[i];
+            int b = (int)((cen[p * 3 + axis] - cmin[axis]) * scale);
+            if (b >= SAH_BINS) b = SAH_BINS - 1;
+            if (b < 0) b = 0;
+            cnt[b]++;
+            for (int vtx = 0; vtx < 3; vtx++)
+                for (int k = 0; k < 3; k++) {
+                    float x = s->v[p * 9 + vtx * 3 + k];
+                    if (x < lo[b][k]) lo[b][k] = x;
+                    if (x > hi[b][k]) hi[b][k] = x;
+                }
+        }
+        float rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        float rarea[SAH_BINS];
+        int64_t rcnt[SAH_BINS], acc = 0;
+        for (int b = SAH_BINS - 1; b > 0; b--) {
+            for (int k = 0; k < 3; k++) {
+                if (lo[b][k] < rlo[k]) rlo[k] = lo[b][k];
+                if (hi[b][k] > rhi[k]) rhi[k] = hi[b][k];
+            }
+            acc += cnt[b];
+            rcnt[b] = acc;
+            rarea[b] = half_area(rlo, rhi);
+        }
+        float llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        int64_t lcnt = 0;
+        for (int b = 0; b < SAH_BINS - 1; b++) {
+            for (int k = 0; k < 3; k++) {
+                if (lo[b][k] < llo[k]) llo[k] = lo[b][k];
+                if (hi[b][k] > lhi[k]) lhi[k] = hi[b][k];
+            }
+            lcnt += cnt[b];
+            if (lcnt == 0 || rcnt[b + 1] == 0) continue;
+            float cost = half_area(llo, lhi) * (float)lcnt + rarea[b + 1] * (float)rcnt[b + 1];
+            if (cost < best_cost) { best_cost = cost; best_axis = axis; best_split = b + 1; }
+        }
+    }
+    float leaf_cost = half_area(nd->bmin, nd->bmax) * (float)count;
+    if (count <= 4 && !(best_cost < leaf_cost)) { nd->left = (int32_t)first; nd->count = (int32_t)count; return; }
+    int64_t half;
+    if (depth >= 48) best_axis = -1;  /* bound the depth (stack, recursion): median splits below 48 levels */
+    if (best_axis >= 0) {
+        /* partition in place by bin (stable enough: ties only decide the tree shape) */
+        float scale = (float)SAH_BINS / (cmax[best_axis] - cmin[best_axis]);
+        int64_t i = first, j = first + count - 1;
+        while (i <= j) {
+            int32_t p = s->prims[i];
+            int b = (int)((cen[p * 3 + best_axis] - cmin[best_axis]) * scale);
+            if (b >= SAH_BINS) b = SAH_BINS - 1;
+            if (b < best_split) i++;
+            else { s->prims[i] = s->prims[j]; s->prims[j] = p; j--; }
+        }
+        half = i - first;
+    } else {
+        /* every centroid coincides (or too deep): a median split on the widest axis */
+        int ax = 0;
+        if (cmax[1] - cmin[1] > cmax[ax] - cmin[ax]) ax = 1;
+        if (cmax[2] - cmin[2] > cmax[ax] - cmin[ax]) ax = 2;
+        g_sort.cen = cen; g_sort.axis = ax;
+        qsort(&s->prims[first], (size_t)count, sizeof(int32_t), cmp_prim);
+        half = count / 2;
+    }
+    if (half <= 0 || half >= count) half = count / 2;
     int64_t l = s->nnodes;
     s->nnodes += 2;
     nd->left = (int32_t)l;
     nd->count = 0;
-    build_node(s, cen, l, first, half);
-    build_node(s, cen, l + 1, first + half, count - half);
+    build_node(s, cen, l, first, half, depth + 1);
+    build_node(s, cen, l + 1, first + half, count - half, depth + 1);
 }
 
 void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nvert, int64_t ntri,
@@ -331,7 +434,7 @@ void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nver
         for (int64_t t = 0; t < ntri; t++) s->prims[t] = (int32_t)t;
         s->nodes = (onode*)malloc(sizeof(onode) * (size_t)(2 * ntri + 1));
         s->nnodes = 1;
-        build_node(s, cen, 0, 0, ntri);
+        build_node(s, cen, 0, 0, ntri, 0);
         free(cen);
     }
     return s;
@@ -379,6 +482,29 @@ static inline void wray_setup(wray* r) {
 /* Returns 1 and t/u/v when the triangle is hit with t in [tmin, tmax]. */
 static inline int woop_test(const wray* r, const float* tv, float tmin, float tmax,
                             float* t_out, float* u_out, float* v_out) {
+#ifdef ORACLE_ALT_TRI
+    /* Moller-Trumbore, barycentrics in the same p = (1-u-v) v0 + u v1 + v v2 convention */
+    {
+        const float e1[3] = {tv[3] - tv[0], tv[4] - tv[1], tv[5] - tv[2]};
+        const float e2[3] = {tv[6] - tv[0], tv[7] - tv[1], tv[8] - tv[2]};
+        const float pv[3] = {r->d[1] * e2[2] - r->d[2] * e2[1], r->d[2] * e2[0] - r->d[0] * e2[2],
+                             r->d[0] * e2[1] - r->d[1] * e2[0]};
+        const float det = (e1[0] * pv[0] + e1[1] * pv[1]) + e1[2] * pv[2];
+        if (det == 0.0f) return 0;
+        const float inv = 1.0f / det;
+        const float tvec[3] = {r->o[0] - tv[0], r->o[1] - tv[1], r->o[2] - tv[2]};
+        const float u = ((tvec[0] * pv[0] + tvec[1] * pv[1]) + tvec[2] * pv[2]) * inv;
+        if (u < 0.0f || u > 1.0f) return 0;
+        const float q[3] = {tvec[1] * e1[2] - tvec[2] * e1[1], tvec[2] * e1[0] - tvec[0] * e1[2],
+                            tvec[0] * e1[1] - tvec[1] * e1[0]};
+        const float v = ((r->d[0] * q[0] + r->d[1] * q[1]) + r->d[2] * q[2]) * inv;
+        if (v < 0.0f || u + v > 1.0f) return 0;
+        const float t = ((e2[0] * q[0] + e2[1] * q[1]) + e2[2] * q[2]) * inv;
+        if (!(t >= tmin && t <= tmax)) return 0;
+        *t_out = t; *u_out = u; *v_out = v;
+        return 1;
+    }
+#endif
     float A[3], B[3], C[3];
     for (int k = 0; k < 3; k++) {
         A[k] = tv[k] - r->o[k];
@@ -452,7 +578,7 @@ static void trace(const oscene* s, const wray* r, float tmin, float tmax, int cl
         }
         return;
     }
-    int32_t stack[128];
+    int32_t stack[256];
     int sp = 0;
     stack[sp++] = 0;
     while (sp) {

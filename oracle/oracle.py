@@ -13,7 +13,8 @@ from ctypes import POINTER, c_float, c_int32, c_int64, c_uint32, c_uint64, c_voi
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+# ORACLE_LIB: another build of the same oracle (tools/sanitize.sh's ASan build)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 PCG32_DEFAULT_STATE = 0x853C49E6748FEA9B
 
 
@@ -30,10 +31,14 @@ def build() -> str:
     return LIB_PATH
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+# oracle.c header: one unpinned arithmetic choice each, and all four at once
+VARIANTS = ("sincos", "rsqrt", "fma", "tri", "all")
+
+
+def _load(path=LIB_PATH):
+    if not os.path.exists(path):
         build()
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     vp = c_void_p
     lib.oracle_scene_create.restype = vp
     lib.oracle_scene_create.argtypes = [vp, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp, c_int32, c_int32]
@@ -53,6 +58,17 @@ def _load():
 
 
 lib = _load()
+_variants = {}
+
+
+def variant(name: str):
+    """liboracle_alt_<name>.so: the oracle with one arithmetic choice swapped
+    (VARIANTS); pass it as OracleScene(..., lib=variant(name))."""
+    if name not in VARIANTS:
+        raise ValueError(f"unknown oracle variant {name!r}; one of {VARIANTS}")
+    if name not in _variants:
+        _variants[name] = _load(os.path.join(HERE, "build", f"liboracle_alt_{name}.so"))
+    return _variants[name]
 
 
 def _p(a):
@@ -83,7 +99,9 @@ def reference_params(width=512, height=512, spp=100, max_depth=2, camera=None, r
 
 
 class OracleScene:
-    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None):
+    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None, lib=None):
+        self.lib = lib if lib is not None else globals()["lib"]
+        lib = self.lib
         self.pt = np.ascontiguousarray(mesh["pos_tri"], dtype=np.int32)
         self.pos = np.ascontiguousarray(mesh["pos"], dtype=np.float32)
         self.nt = None if mesh.get("nrm_tri") is None else np.ascontiguousarray(mesh["nrm_tri"], dtype=np.int32)
@@ -102,8 +120,8 @@ class OracleScene:
             lib.oracle_scene_set_emission(self.h, _p(self.emi), self.emi.shape[0])
 
     def __del__(self):
-        if getattr(self, "h", None) and lib is not None:  # (module teardown at exit)
-            lib.oracle_scene_destroy(self.h)
+        if getattr(self, "h", None) and getattr(self, "lib", None) is not None:  # (module teardown at exit)
+            self.lib.oracle_scene_destroy(self.h)
             self.h = None
 
     def intersect(self, o, d, tmin=None, tmax=None, mask=None, closest=True, nthreads=8, init=None):
@@ -120,7 +138,7 @@ class OracleScene:
             t, u, v = (np.zeros(n, np.float32) for _ in range(3))
         else:
             tri, t, u, v = (np.array(x, copy=True) for x in init)
-        lib.oracle_intersect(self.h, _p(o[0]), _p(o[1]), _p(o[2]), _p(d[0]), _p(d[1]), _p(d[2]), _p(tmin), _p(tmax),
+        self.lib.oracle_intersect(self.h, _p(o[0]), _p(o[1]), _p(o[2]), _p(d[0]), _p(d[1]), _p(d[2]), _p(tmin), _p(tmax),
                              _p(mask), mask.size, _p(tri), _p(t), _p(u), _p(v), n, 1 if closest else 0, nthreads)
         return tri, t, u, v
 
@@ -128,7 +146,7 @@ class OracleScene:
         rows = np.arange(params.height, dtype=np.int32) if rows is None else np.ascontiguousarray(rows, np.int32)
         film = np.zeros((3, rows.size, params.width), np.float32)
         casts = c_uint64(0)
-        rc = lib.oracle_render(self.h, ctypes.byref(params), _p(rows), rows.size, _p(film), nthreads,
+        rc = self.lib.oracle_render(self.h, ctypes.byref(params), _p(rows), rows.size, _p(film), nthreads,
                                ctypes.byref(casts))
         if rc != 0:
             raise RuntimeError(f"oracle_render failed: {rc}")

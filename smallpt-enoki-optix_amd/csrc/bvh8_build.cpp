@@ -20,9 +20,9 @@ struct Kid {
     int32_t code;  // BVH2 child code: >= 0 inner node, < 0 leaf ~(first << 3 | count - 1)
     uint32_t ntri = 0;  // triangles in the subtree
     bool leaf = false;  // becomes a BVH8 leaf (all its <= 3 triangles) rather than a BVH8 node
-    float area() const {
-        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    double area() const {  // double: boxes near FLT_MAX would overflow a float area
+        const double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
     }
 };
 
@@ -101,7 +101,7 @@ struct Collapser {
         dist.assign(nn * 9, INFINITY);
         take.assign(nn * 9, 0);
         split.assign(nn * 9, 0);
-        std::vector<float> area(nn, 0.0f);
+        std::vector<double> area(nn, 0.0);
         area[root] = root_kid.area();
         // post-order over inner nodes (parents before children in a pre-order list)
         std::vector<int32_t> order, stack{root};
@@ -122,18 +122,20 @@ struct Collapser {
             const Kid l = child(n, 0), r = child(n, 1);
             double* C = &cost[(size_t)n * 9];
             double* D = &dist[(size_t)n * 9];
-            for (int i = 2; i <= 8; i++)
+            for (int i = 2; i <= 8; i++) {
+                split[(size_t)n * 9 + i] = 1;  // a valid share even when every cost is inf / NaN
                 for (int k = 1; k < i; k++) {
                     const double v = kid_cost(l, k) + kid_cost(r, i - k);
                     if (v < D[i]) { D[i] = v; split[(size_t)n * 9 + i] = (uint8_t)k; }
                 }
+            }
             Kid self;
             self.code = n;
             self.ntri = ntri2[n];
             const double lc = self.ntri <= 3 ? (double)area[n] * c_prim * (double)self.ntri : INFINITY;
             const double ic = (double)area[n] * c_node + D[8];
             C[1] = std::min(lc, ic);
-            take[(size_t)n * 9 + 1] = lc <= ic ? 1 : 0;
+            take[(size_t)n * 9 + 1] = (self.ntri <= 3 && lc <= ic) ? 1 : 0;
             for (int i = 2; i <= 8; i++) {
                 take[(size_t)n * 9 + i] = C[i - 1] <= D[i] ? 1 : 0;
                 C[i] = std::min(C[i - 1], D[i]);
@@ -177,7 +179,7 @@ struct Collapser {
         // candidates (largest first) to fill the 8 slots.
         while (mode < 3 && kids.size() < 8) {
             int best = -1;
-            float best_area = -1.0f;
+            double best_area = -1.0;
             for (size_t i = 0; i < kids.size(); i++)
                 if (kids[i].code >= 0 && !leafable(kids[i]) && kids[i].area() > best_area) {
                     best_area = kids[i].area();
@@ -248,10 +250,12 @@ struct Collapser {
         for (int a = 0; a < 3; a++) {
             double ext = (double)hi[a] - (double)lo[a];
             int e = -100;
-            if (ext > 0.0) {
+            if (!(ext <= 1e300)) {
+                e = 127;  // infinite (or NaN) extent: the widest step; such triangles are never hit
+            } else if (ext > 0.0) {
                 e = (int)std::ceil(std::log2(ext / 255.0));
                 while (std::ldexp(255.0, e) < ext) e++;
-                e = std::max(e, -100);
+                e = std::min(std::max(e, -100), 127);
             }
             ebias[a] = e + 127;
             std::memcpy(&w[a], &lo[a], 4);

@@ -679,6 +679,36 @@ spt_status spt_scene_get_stats(spt_scene sc, spt_scene_stats* out) {
     return SPT_OK;
 }
 
+spt_status spt_bvh_build_stats(const float* tv, uint64_t ntri, const spt_config* cfg_in, spt_scene_stats* out) {
+    if (!out || (ntri > 0 && !tv)) return fail(SPT_ERR_INVALID, "spt_bvh_build_stats: NULL argument");
+    if (ntri >= kMaxTriangles) return fail(SPT_ERR_LIMIT, "spt_bvh_build_stats: %llu triangles exceeds 2^28",
+                                           (unsigned long long)ntri);
+    spt_config cfg;
+    if (cfg_in) cfg = *cfg_in;
+    else spt_default_config(&cfg);
+    spt_status st = check_config(cfg);
+    if (st) return st;
+    spt_scene_stats ss{};
+    const double t0 = now_ms();
+    if (cfg.bvh_width == 8) {
+        const Bvh8BuildResult b = build_bvh8(tv, ntri, cfg.collapse == 1);
+        ss.nodes = b.nodes.size() / 20; ss.leaves = b.leaves; ss.max_depth = b.depth; ss.max_leaf = 3;
+        ss.sah_cost = b.sah_cost;
+        if (b.slot2tri.size() != ntri) return fail(SPT_ERR_HIP, "spt_bvh_build_stats: BVH8 lost triangles");
+    } else {
+        const BvhBuildResult b = build_bvh(tv, ntri);
+        ss.nodes = b.nodes.size() / 16; ss.leaves = b.leaves; ss.max_depth = b.max_depth; ss.max_leaf = b.max_leaf;
+        ss.sah_cost = b.sah_cost;
+        if (b.slot2tri.size() != ntri) return fail(SPT_ERR_HIP, "spt_bvh_build_stats: BVH2 lost triangles");
+    }
+    ss.ntri = ntri;
+    ss.bvh_width = cfg.bvh_width;
+    ss.builder = SPT_BUILD_HOST_SAH;
+    ss.build_ms = now_ms() - t0;
+    *out = ss;
+    return SPT_OK;
+}
+
 spt_status spt_scene_destroy(spt_scene sc) {
     if (!sc) return SPT_OK;
     sc->release();

@@ -280,7 +280,8 @@ __global__ __launch_bounds__(kBlock) void dp_kernel(const float4* __restrict__ l
     const float ic = area * kCNode + D[8];
     DpNode out;
     out.cost[0] = fminf(lc, ic);
-    uint32_t take = lc <= ic ? 2u : 0u;
+    // a leaf only when it may be one (with overflowing areas both costs are inf)
+    uint32_t take = (ntris[n] <= kLeafMaxTris && lc <= ic) ? 2u : 0u;
     for (int i = 2; i <= 8; i++) {
         if (out.cost[i - 2] <= D[i]) take |= 1u << i;
         out.cost[i - 1] = fminf(out.cost[i - 2], D[i]);
@@ -439,10 +440,12 @@ __global__ __launch_bounds__(kBlock) void collapse_emit_kernel(EmitArgs a) {
     for (int ax = 0; ax < 3; ax++) {
         const double ext = (double)hi[ax] - (double)lo[ax];
         int ex = -100;
-        if (ext > 0.0) {
+        if (!(ext <= 1e300)) {
+            ex = 127;  // infinite (or NaN) extent: the widest step; such triangles are never hit
+        } else if (ext > 0.0) {
             ex = (int)ceil(log2(ext / 255.0));
             while (ldexp(255.0, ex) < ext) ex++;
-            ex = max(ex, -100);
+            ex = min(max(ex, -100), 127);
         }
         ebias[ax] = ex + 127;
         w[ax] = __builtin_bit_cast(uint32_t, lo[ax]);

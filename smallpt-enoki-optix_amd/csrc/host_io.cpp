@@ -15,16 +15,19 @@
 #include <vector>
 
 #include "../../include/spt.h"
+#include "host_error.h"
 
 namespace {
 
 struct Idx { int v, t, n; };
 
 bool parse_index(const char*& p, int nv, int nt, int nn, Idx& out) {
+    // 1-based, or relative to the elements read so far; 0 and anything
+    // beyond int range are invalid (-2; the caller range-checks the rest)
     auto fix = [](long i, int n) -> int {
-        if (i > 0) return (int)(i - 1);
-        if (i < 0) return (int)(n + i);
-        return -2;  // 0 is invalid in OBJ
+        if (i > 0) return i <= 0x7fffffffL ? (int)(i - 1) : -2;
+        if (i < 0) return i >= -(long)n ? (int)(n + i) : -2;
+        return -2;
     };
     char* end;
     long v = std::strtol(p, &end, 10);
@@ -89,10 +92,10 @@ T* dup(const std::vector<T>& v) {
 extern "C" {
 
 spt_status spt_obj_load(const char* path, spt_mesh* out) {
-    if (!path || !out) return SPT_ERR_INVALID;
+    if (!path || !out) return spt_set_error(SPT_ERR_INVALID, "spt_obj_load: NULL argument");
     std::memset(out, 0, sizeof(*out));
     FILE* f = std::fopen(path, "r");
-    if (!f) return SPT_ERR_IO;
+    if (!f) return spt_set_error(SPT_ERR_IO, "spt_obj_load: cannot open %s: %s", path, std::strerror(errno));
     std::string dir(path);
     size_t slash = dir.find_last_of('/');
     dir = slash == std::string::npos ? std::string() : dir.substr(0, slash + 1);
@@ -106,7 +109,9 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
     size_t cap = 0;
     ssize_t len;
     bool bad = false;
+    long lineno = 0;
     while ((len = getline(&line, &cap, f)) >= 0) {
+        lineno++;
         const char* p = line;
         while (*p == ' ' || *p == '\t') p++;
         if (p[0] == 'v' && (p[1] == ' ' || p[1] == '\t')) {
@@ -129,7 +134,7 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
                 while (*p == ' ' || *p == '\t') p++;
                 if (*p == '\0' || *p == '\n' || *p == '\r' || *p == '#') break;
                 Idx ix;
-                if (!parse_index(p, nv, ntc, nn, ix)) { bad = true; break; }
+                if (!parse_index(p, nv, ntc, nn, ix) || ix.t == -2 || ix.n == -2) { bad = true; break; }
                 poly.push_back(ix);
                 while (*p && *p != ' ' && *p != '\t' && *p != '\n' && *p != '\r') p++;
             }
@@ -160,11 +165,15 @@ spt_status spt_obj_load(const char* path, spt_mesh* out) {
     }
     std::free(line);
     std::fclose(f);
-    if (bad) return SPT_ERR_INVALID;
+    if (bad) return spt_set_error(SPT_ERR_INVALID, "spt_obj_load: %s:%ld: bad face index", path, lineno);
     // Index range check (tinyobj would hand out-of-range indices through).
-    const int nv = (int)(pos.size() / 3);
+    const long nv = (long)(pos.size() / 3), nvt = (long)(tc.size() / 2), nvn = (long)(nrm.size() / 3);
     for (int32_t i : pt)
-        if (i < 0 || i >= nv) return SPT_ERR_INVALID;
+        if (i < 0 || i >= nv) return spt_set_error(SPT_ERR_INVALID, "spt_obj_load: %s: vertex index %d of %ld", path, i + 1, nv);
+    for (int32_t i : tt)
+        if (i < -1 || i >= nvt) return spt_set_error(SPT_ERR_INVALID, "spt_obj_load: %s: texcoord index %d of %ld", path, i + 1, nvt);
+    for (int32_t i : nt)
+        if (i < -1 || i >= nvn) return spt_set_error(SPT_ERR_INVALID, "spt_obj_load: %s: normal index %d of %ld", path, i + 1, nvn);
 
     // Material table: [0] = default, then one entry per .mtl material (its Kd).
     std::vector<float> kd_all(3, 1.0f);
@@ -198,9 +207,9 @@ void spt_mesh_free(spt_mesh* m) {
 }
 
 spt_status spt_pfm_write(const char* path, const float* r, const float* g, const float* b, uint32_t w, uint32_t h) {
-    if (!path || !r || !g || !b) return SPT_ERR_INVALID;
+    if (!path || !r || !g || !b) return spt_set_error(SPT_ERR_INVALID, "spt_pfm_write: NULL argument");
     FILE* f = std::fopen(path, "wb");
-    if (!f) return SPT_ERR_IO;
+    if (!f) return spt_set_error(SPT_ERR_IO, "spt_pfm_write: cannot open %s: %s", path, std::strerror(errno));
     std::fprintf(f, "PF\n%u %u\n-1\n", w, h);
     std::vector<float> row((size_t)w * 3);
     for (uint32_t y = 0; y < h; y++) {
@@ -212,10 +221,10 @@ spt_status spt_pfm_write(const char* path, const float* r, const float* g, const
         }
         if (std::fwrite(row.data(), sizeof(float), row.size(), f) != row.size()) {
             std::fclose(f);
-            return SPT_ERR_IO;
+            return spt_set_error(SPT_ERR_IO, "spt_pfm_write: short write to %s", path);
         }
     }
-    return std::fclose(f) == 0 ? SPT_OK : SPT_ERR_IO;
+    return std::fclose(f) == 0 ? SPT_OK : spt_set_error(SPT_ERR_IO, "spt_pfm_write: closing %s failed", path);
 }
 
 }  // extern "C"

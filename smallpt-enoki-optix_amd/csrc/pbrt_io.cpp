@@ -472,7 +472,10 @@ class Parser {
             if (!P || P->nums.size() % 3) return fail("trianglemesh needs \"point P\"");
             c.p = P->nums;
             if (I) {
-                for (double v : I->nums) c.idx.push_back((int32_t)v);
+                for (double v : I->nums) {
+                    // -1 is out of range for every mesh; UB-free for any double
+                    c.idx.push_back(v >= -2147483648.0 && v < 2147483648.0 ? (int32_t)v : -1);
+                }
             } else if (c.p.size() == 9) {
                 c.idx = {0, 1, 2};
             } else {
@@ -576,8 +579,11 @@ class Parser {
                 Token n = lex.next();
                 ParamList pl;
                 if (n.kind != Token::STRING || !params(pl)) return err.empty() ? fail("Film needs a type") : false;
-                info.xres = (uint32_t)pl.num("xresolution", 640);
-                info.yres = (uint32_t)pl.num("yresolution", 480);
+                const double xr = pl.num("xresolution", 640), yr = pl.num("yresolution", 480);
+                if (!(xr >= 1.0 && xr <= 1048576.0 && yr >= 1.0 && yr <= 1048576.0))
+                    return fail("Film resolution %g x %g outside [1, 2^20]", xr, yr);
+                info.xres = (uint32_t)xr;
+                info.yres = (uint32_t)yr;
             } else if (d == "WorldBegin") {
                 gs.ctm = Mat4::identity();
                 coord_sys["world"] = gs.ctm;
@@ -852,7 +858,10 @@ bool Parser::read_ply(const std::string& path, Chunk& c) {
                 if ((int)k == ilist) poly.clear();
                 for (int64_t j = 0; j < (int64_t)cnt && r.ok; j++) {
                     const double x = r.read(pr.type);
-                    if ((int)k == ilist) poly.push_back((int32_t)x);
+                    if ((int)k == ilist) {
+                        if (!(x >= -2147483648.0 && x < 2147483648.0)) { r.ok = false; break; }
+                        poly.push_back((int32_t)x);
+                    }
                 }
             }
             if (!r.ok) break;

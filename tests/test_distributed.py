@@ -1,4 +1,4 @@
-"""N>1 path on CPU: world_size-2 gloo processes, each renders its interleaved
+"""N>1 path on CPU: world_size-2, 3 and 8 gloo processes, each renders its interleaved
 row-group tile (with the CPU oracle standing in for the GPU renderer) and the
 package's TileGather gathers and assembles the framebuffer on rank 0; the
 result must equal the single-process render bit for bit."""
@@ -43,7 +43,7 @@ def _worker(rank, world, port, rpg, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rpg", [(2, 1), (2, 4), (3, 8)])
+@pytest.mark.parametrize("world,rpg", [(2, 1), (2, 4), (3, 8), (8, 1), (8, 2)])
 def test_tile_gather_matches_single_render(tmp_path, world, rpg):
     import oracle as O
     from sptamd import scenes

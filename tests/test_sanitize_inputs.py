@@ -1,0 +1,200 @@
+"""Hostile and malformed inputs for the host code that reads untrusted files
+and builds the acceleration structure (VERDICT r1 "do this" 7): the OBJ
+reader (load_meshes, main.cpp:141-251), the pbrt-v3 + PLY reader
+(csrc/pbrt_io.cpp) and the host BVH2 / BVH8 builders (spt_bvh_build_stats).
+Each case must end in SPT_OK with in-range indices or a clean error code —
+never a crash.  tools/sanitize.sh runs this file (with test_host.py,
+test_pbrt.py and test_oracle.py) against an ASan + UBSan build, where any
+out-of-bounds access or undefined behaviour aborts the run
+(profiles/sanitize_r02.log)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import sptamd
+from sptamd import _lib, scenes
+
+
+def _load(fn, path):
+    m = _lib.Mesh()
+    info = _lib.PbrtInfo()
+    st = fn(path.encode(), ctypes.byref(m)) if fn is _lib.lib.spt_obj_load else \
+        fn(path.encode(), ctypes.byref(m), ctypes.byref(info))
+    try:
+        if st == 0:
+            mesh = scenes._mesh_from_c(m)
+            n = len(mesh["pos"])
+            assert mesh["pos_tri"].size == 0 or (mesh["pos_tri"].min() >= 0 and mesh["pos_tri"].max() < n)
+            nn = len(mesh["nrm"])
+            if mesh["nrm_tri"].size and nn:
+                assert mesh["nrm_tri"].min() >= -1 and mesh["nrm_tri"].max() < nn
+        else:
+            assert st in (1, 5, 6), st
+            assert _lib.lib.spt_last_error()
+    finally:
+        _lib.lib.spt_mesh_free(ctypes.byref(m))
+    return st
+
+
+def _mutations(data: bytes, seed: int, n: int):
+    rng = np.random.default_rng(seed)
+    for i in range(n):
+        b = bytearray(data)
+        kind = i % 4
+        if kind == 0 and len(b) > 1:          # truncate
+            b = b[: int(rng.integers(0, len(b)))]
+        elif kind == 1:                       # flip bytes
+            for _ in range(int(rng.integers(1, 8))):
+                if b:
+                    b[int(rng.integers(0, len(b)))] = int(rng.integers(0, 256))
+        elif kind == 2 and len(b) > 2:        # delete a span
+            a = int(rng.integers(0, len(b) - 1))
+            del b[a: a + int(rng.integers(1, 64))]
+        else:                                 # duplicate a span
+            a = int(rng.integers(0, max(1, len(b))))
+            b[a:a] = b[a: a + int(rng.integers(1, 64))]
+        yield bytes(b)
+
+
+OBJ_CASES = [
+    "",
+    "v 0 0 0\nv 1 0 0\nf 1 2 3\n",                    # index past the end
+    "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 -4\n",          # negative past the start
+    "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2\n",             # a face of two vertices
+    "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1/1/1 2/2/2 3/3/3\n",  # vt / vn indices without vt / vn
+    "v 0 0\nf 1 1 1\n",                               # short vertex
+    "vn 0 0\nvt\nv nan inf -inf\nf 1 1 1\n",
+    "v 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3 " + "1 " * 5000 + "\n",  # a huge polygon
+    "v 0 0 0\n" * 3 + "f 2147483647 2 3\nf -2147483648 1 2\nf 99999999999999999999 1 2\n",
+    "mtllib /nonexistent/x.mtl\nusemtl a\nv 0 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n",
+    "\x00\x01\x02 binary garbage \xff\n" * 4,
+    "v " + "9" * 5000 + " 0 0\nf 1 1 1\n",
+]
+
+
+@pytest.mark.parametrize("i", range(len(OBJ_CASES)))
+def test_obj_reader_hostile(tmp_path, i):
+    path = tmp_path / "x.obj"
+    path.write_bytes(OBJ_CASES[i].encode("latin-1"))
+    _load(_lib.lib.spt_obj_load, str(path))
+
+
+def test_obj_reader_mutations(tmp_path):
+    m = scenes.mitsuba_synth(detail=0.05)
+    src = tmp_path / "src.obj"
+    scenes.write_obj(str(src), m)
+    data = src.read_bytes()
+    ok = 0
+    for k, b in enumerate(_mutations(data, 1, 60)):
+        p = tmp_path / f"m{k}.obj"
+        p.write_bytes(b)
+        ok += _load(_lib.lib.spt_obj_load, str(p)) == 0
+    assert ok > 0
+
+
+PBRT_CASES = [
+    "",
+    "WorldBegin\nAttributeEnd\nWorldEnd\n",
+    "WorldBegin\nShape \"trianglemesh\" \"integer indices\" [0 1 7] \"point P\" [0 0 0 1 0 0 0 1 0]\nWorldEnd\n",
+    "WorldBegin\nShape \"trianglemesh\" \"integer indices\" [0 1] \"point P\" [0 0 0 1 0 0 0 1 0]\nWorldEnd\n",
+    "WorldBegin\nShape \"trianglemesh\" \"integer indices\" [0 1 2] \"point P\" [0 0 0 1 0]\nWorldEnd\n",
+    "WorldBegin\nShape \"trianglemesh\" \"integer indices\" [0 1 2 \"point P\" [0 0 0 1 0 0 0 1 0]\nWorldEnd\n",
+    "WorldBegin\nInclude \"/nonexistent/file.pbrt\"\nWorldEnd\n",
+    "WorldBegin\nObjectInstance \"never\"\nWorldEnd\n",
+    "WorldBegin\nObjectBegin \"a\"\nObjectBegin \"b\"\nWorldEnd\n",
+    "Translate 1 2\nWorldBegin\nWorldEnd\n",
+    "LookAt 0 0 0 0 0 0 0 0 0\nCamera \"perspective\" \"float fov\" [ -5 ]\nWorldBegin\nWorldEnd\n",
+    "Film \"image\" \"integer xresolution\" [ -1 ] \"integer yresolution\" [ 4000000000 ]\nWorldBegin\nWorldEnd\n",
+    "WorldBegin\nShape \"plymesh\" \"string filename\" \"missing.ply\"\nWorldEnd\n",
+    "WorldBegin\nNamedMaterial \"undefined\"\nShape \"sphere\"\nWorldEnd\n",
+    "\"unterminated string\nWorldBegin\n",
+    "WorldBegin\n" + "AttributeBegin\n" * 2000 + "WorldEnd\n",
+    "Transform [1 2 3]\nConcatTransform [" + "1 " * 20 + "]\n",
+    "WorldBegin\nShape \"trianglemesh\" \"integer indices\" [0 1 2] \"point P\" [0 0 0 1 0 0 0 1 0] "
+    "\"normal N\" [0 1 0] \"float uv\" [0 0 1]\nWorldEnd\n",
+]
+
+
+@pytest.mark.parametrize("i", range(len(PBRT_CASES)))
+def test_pbrt_reader_hostile(tmp_path, i):
+    path = tmp_path / "x.pbrt"
+    path.write_text(PBRT_CASES[i])
+    _load(_lib.lib.spt_pbrt_load, str(path))
+
+
+PLY_HEADERS = [
+    b"ply\nformat binary_little_endian 1.0\nelement vertex 3\nproperty float x\nproperty float y\n"
+    b"property float z\nelement face 1\nproperty list uchar int vertex_indices\nend_header\n",
+    b"ply\nformat binary_big_endian 1.0\nelement vertex 1000000000\nproperty float x\nproperty float y\n"
+    b"property float z\nelement face 1\nproperty list uchar int vertex_indices\nend_header\n",
+    b"ply\nformat ascii 1.0\nelement vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+    b"element face 1\nproperty list uchar int vertex_indices\nend_header\n0 0 0\n1 0 0\n",
+    b"ply\nformat binary_little_endian 1.0\nelement vertex 3\nproperty double x\nproperty short y\n"
+    b"property float z\nelement face 2\nproperty list int int vertex_indices\nend_header\n",
+    b"ply\nformat ascii 1.0\nelement face 1\nproperty list uchar int vertex_indices\nelement vertex 3\n"
+    b"property float x\nproperty float y\nproperty float z\nend_header\n3 0 1 2\n0 0 0\n1 0 0\n0 1 0\n",
+    b"ply\nformat ascii 1.0\nelement vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+    b"element face 1\nproperty list uchar int vertex_indices\nend_header\n0 0 0\n1 0 0\n0 1 0\n255 0 1 2\n",
+]
+
+
+@pytest.mark.parametrize("i", range(len(PLY_HEADERS)))
+def test_ply_hostile(tmp_path, i):
+    body = PLY_HEADERS[i]
+    if b"binary_little" in body:
+        body += np.zeros(9, "<f4").tobytes() + bytes([3]) + np.array([0, 1, 9], "<i4").tobytes()[:7]  # truncated
+    (tmp_path / "m.ply").write_bytes(body)
+    p = tmp_path / "s.pbrt"
+    p.write_text('WorldBegin\nShape "plymesh" "string filename" "m.ply"\nWorldEnd\n')
+    _load(_lib.lib.spt_pbrt_load, str(p))
+
+
+def test_pbrt_mutations(tmp_path):
+    m = scenes.mitsuba_synth(detail=0.05)
+    src = str(tmp_path / "src.pbrt")
+    scenes.write_pbrt(src, m, binary=True)
+    plys = [f for f in os.listdir(tmp_path) if f.endswith(".ply")]
+    assert plys
+    text = open(src, "rb").read()
+    ply = (tmp_path / plys[0]).read_bytes()
+    ok = 0
+    for k, (t, pl) in enumerate(zip(_mutations(text, 2, 30), _mutations(ply, 3, 30))):
+        d = tmp_path / f"case{k}"
+        d.mkdir()
+        for f in plys:
+            (d / f).write_bytes((tmp_path / f).read_bytes())
+        (d / plys[0]).write_bytes(pl if k % 2 else ply)
+        (d / "s.pbrt").write_bytes(t if k % 2 == 0 else text)
+        ok += _load(_lib.lib.spt_pbrt_load, str(d / "s.pbrt")) == 0
+    assert ok > 0
+
+
+def _soups():
+    rng = np.random.default_rng(9)
+    yield "one", np.array([[0, 0, 0, 1, 0, 0, 0, 1, 0]], np.float32)
+    yield "coincident", np.zeros((300, 9), np.float32)
+    yield "collinear", np.stack([np.linspace(0, 1, 500)] * 9, 1).astype(np.float32)
+    yield "random", rng.normal(size=(20000, 9)).astype(np.float32)
+    yield "huge", (rng.normal(size=(2000, 9)) * 1e30).astype(np.float32)
+    yield "tiny", (rng.normal(size=(2000, 9)) * 1e-30).astype(np.float32)
+    g = rng.normal(size=(3000, 9)).astype(np.float32)
+    g[::7, 0] = np.inf
+    g[::11, 4] = np.nan
+    yield "nonfinite", g
+    m = scenes.city_synth(60_000)
+    yield "city", np.asarray(m["pos"], np.float32)[np.asarray(m["pos_tri"])].reshape(-1, 9)
+
+
+@pytest.mark.parametrize("name,tv", list(_soups()), ids=lambda x: x if isinstance(x, str) else "")
+def test_host_bvh_builders(name, tv):
+    for width, collapse in ((8, 0), (8, 1), (2, 0)):
+        cfg = sptamd.default_config()
+        cfg.bvh_width, cfg.collapse = width, collapse
+        st = _lib.SceneStats()
+        tv = np.ascontiguousarray(tv, np.float32)
+        rc = _lib.lib.spt_bvh_build_stats(tv.ctypes.data, tv.shape[0], ctypes.byref(cfg), ctypes.byref(st))
+        assert rc == 0, _lib.lib.spt_last_error()
+        assert st.ntri == tv.shape[0] and st.nodes >= 1 and st.bvh_width == width
+        assert st.max_depth < 200

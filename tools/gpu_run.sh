@@ -24,7 +24,8 @@ run() {  # name timeout cmd...
 for s in "$@"; do
   case "$s" in
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
-    tests) run tests 900 python -m pytest tests -m gpu -q -x ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread ;;
+    testsv) run testsv 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
     tests2) run tests2 900 env SPT_BVH=2 python -m pytest tests -m gpu -q -x ;;
     testsgb) run testsgb 900 env SPT_BUILD=gpu python -m pytest tests -m gpu -q -x ;;
@@ -32,14 +33,15 @@ for s in "$@"; do
     bench1gq) run bench1gq 600 env SPT_BUILD=gpu python bench.py --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
-    bench2|bench3|bench4) run $s 600 python bench.py --config ${s#bench} --steps 2 --warmup 1 ;;
+    bench0|bench2|bench3|bench4) run $s 600 python bench.py --config ${s#bench} --steps 2 --warmup 1 ;;
     bench2q|bench3q|bench4q) c=${s#bench}; run $s 600 python bench.py --config ${c%q} --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchwf) for wf in ${WFS:-1048576 4194304 8388608}; do run benchwf$wf 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --wavefront $wf; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     prof2|prof4) run $s 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$s -o run --output-format csv -- python bench.py --config ${s#prof} --steps 1 --warmup 1 --no-cpu-baseline ;;
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pmc) run pmc 900 bash tools/pmc_isect.sh gpurun_out/pmc ;;
+    pmc|pmc1|pmc2|pmc3|pmc4) c=${s#pmc}; run $s 900 env CONFIG=${c:-1} bash tools/pmc_isect.sh gpurun_out/pmc ;;
+    prof1s) run prof1s 600 env SPT_STREAMS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1s -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
     tilesim) run tilesim 400 python tools/tile_sim.py ;;
     tilesimt) run tilesimt 400 python tools/tile_sim.py --timing ;;
