@@ -54,20 +54,18 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// 68 B per path: q0, q1, q2 (16 B each), rng_hi (4 B), rad (16 B, emitters)
-constexpr size_t kPathBytes = 3 * 16 + 4 + 16;
+// Path queue planes (spt_internal.h PathQueue): 2 (unit), 3 (albedo) or 4
+// (emitters) 16-B quads per path.
 constexpr size_t kHitBytes = 16;
 
-// Planes are `stride` elements apart (stride = cap + pad, see queue_stride);
-// the quad planes first, so each stays 16-B aligned.
-PathQueue carve_queue(char* base, size_t stride) {
+// Planes are `stride` elements apart (stride = cap + pad, see queue_stride).
+PathQueue carve_queue(char* base, size_t stride, uint32_t planes) {
     PathQueue q;
     float4* f4 = (float4*)base;
-    q.q0 = f4;
-    q.q1 = f4 + stride;
-    q.q2 = f4 + 2 * stride;
-    q.rad = f4 + 3 * stride;
-    q.rng_hi = (uint32_t*)(f4 + 4 * stride);
+    q.q1 = f4;
+    q.q2 = f4 + stride;
+    q.q0 = planes > 2 ? f4 + 2 * stride : nullptr;
+    q.rad = planes > 3 ? f4 + 3 * stride : nullptr;
     return q;
 }
 
@@ -97,6 +95,7 @@ constexpr int kMaxStreams = 4;
 struct Sub {
     size_t cap = 0;
     uint32_t pad = 0;                   // plane pad the queues were carved with
+    uint32_t planes = 0;                // 16-B planes per path allocated
     char* qa = nullptr;
     char* qb = nullptr;
     char* hits = nullptr;
@@ -109,9 +108,10 @@ struct Sub {
 
 struct Workspace {
     Sub sub[kMaxStreams];
-    size_t film_cap = 0, jump_cap = 0;
-    float* film = nullptr;
-    PcgJump* jumps = nullptr;
+    size_t film_cap = 0, acc_cap = 0, jump_cap = 0;
+    char* film = nullptr;               // per-sample contributions of a chunk (bytes or RGB floats)
+    float* acc = nullptr;               // [3][P] running sum across chunks
+    PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
     Stats* stats = nullptr;
     hipEvent_t fork_ev = nullptr;
@@ -125,7 +125,7 @@ struct Workspace {
             if (b.join_ev) (void)hipEventDestroy(b.join_ev);
             if (b.stream) (void)hipStreamDestroy(b.stream);
         }
-        hfree(film); hfree(jumps); hfree(stats);
+        hfree(film); hfree(acc); hfree(jumps); hfree(stats);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         for (auto e : events) (void)hipEventDestroy(e);
         *this = Workspace();
@@ -149,6 +149,7 @@ struct spt_scene_t {
     uint32_t nmat = 1;
     float* emission = nullptr;
     uint32_t nemit = 0;
+    bool albedo_unit = true;  // every albedo entry is exactly 1 (the reference's case)
     uint32_t stack_depth = 1;
     spt_scene_stats stats{};
     Workspace ws;
@@ -206,17 +207,19 @@ Camera make_camera(const spt_render_params& p) {
     return cam;
 }
 
-spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, size_t film_floats, size_t njumps) {
+spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, uint32_t planes, size_t film_bytes,
+                            size_t acc_floats, size_t njumps) {
     for (int k = 0; k < nsub; k++) {
         Sub& b = ws.sub[k];
-        if (cap > b.cap || pad != b.pad) {
+        if (cap > b.cap || pad != b.pad || planes > b.planes) {
             hfree(b.qa); hfree(b.qb); hfree(b.hits);
             b.cap = 0;
-            HIP_TRY(hipMalloc((void**)&b.qa, kPathBytes * queue_stride(cap, pad)));
-            HIP_TRY(hipMalloc((void**)&b.qb, kPathBytes * queue_stride(cap, pad)));
+            HIP_TRY(hipMalloc((void**)&b.qa, (size_t)16 * planes * queue_stride(cap, pad)));
+            HIP_TRY(hipMalloc((void**)&b.qb, (size_t)16 * planes * queue_stride(cap, pad)));
             HIP_TRY(hipMalloc((void**)&b.hits, kHitBytes * cap));
             b.cap = cap;
             b.pad = pad;
+            b.planes = planes;
         }
         if (!b.cnt) HIP_TRY(hipMalloc((void**)&b.cnt, sizeof(Counters)));
         if (!b.host_cnt) HIP_TRY(hipHostMalloc((void**)&b.host_cnt, 2 * sizeof(Counters), hipHostMallocDefault));
@@ -225,11 +228,17 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, s
         if (!b.join_ev) HIP_TRY(hipEventCreateWithFlags(&b.join_ev, hipEventDisableTiming));
         if (k > 0 && !b.stream) HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
     }
-    if (film_floats > ws.film_cap) {
+    if (film_bytes > ws.film_cap) {
         hfree(ws.film);
         ws.film_cap = 0;
-        HIP_TRY(hipMalloc((void**)&ws.film, sizeof(float) * film_floats));
-        ws.film_cap = film_floats;
+        HIP_TRY(hipMalloc((void**)&ws.film, film_bytes));
+        ws.film_cap = film_bytes;
+    }
+    if (acc_floats > ws.acc_cap) {
+        hfree(ws.acc);
+        ws.acc_cap = 0;
+        HIP_TRY(hipMalloc((void**)&ws.acc, sizeof(float) * acc_floats));
+        ws.acc_cap = acc_floats;
     }
     if (njumps > ws.jump_cap) {
         hfree(ws.jumps);
@@ -604,14 +613,19 @@ spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t 
     float* d = nullptr;
     HIP_TRY(hipMalloc((void**)&d, sizeof(float) * 3 * nmat));
     HIP_TRY(hipMemcpy(d, albedo_rgb, sizeof(float) * 3 * nmat, hipMemcpyHostToDevice));
+    std::lock_guard<std::mutex> lk(sc->mu);
     hfree(sc->albedo);
     sc->albedo = d;
     sc->nmat = nmat;
+    bool unit = true;
+    for (uint32_t i = 0; i < 3 * nmat; i++) unit = unit && albedo_rgb[i] == 1.0f;
+    sc->albedo_unit = unit;
     return SPT_OK;
 }
 
 spt_status spt_scene_set_emission(spt_scene sc, const float* emission_rgb, uint32_t nmat) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_emission: NULL scene");
+    std::lock_guard<std::mutex> lk(sc->mu);
     hfree(sc->emission);
     sc->nemit = 0;
     if (!emission_rgb || nmat == 0) return SPT_OK;  // no emitters
@@ -833,14 +847,20 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
-    // Per-sample contribution film [chunk][3][P], at most film_budget_bytes
-    // (4 GiB) per chunk; chunks carry the running sum in acc.
+    // What a path carries (spt_internal.h PathMode): the reference's case
+    // (every albedo 1, no emitters) needs only the ray and an escaped flag.
+    const int mode = sc->emission ? kModeEmit : (sc->albedo_unit ? kModeUnit : kModeAlbedo);
+    const uint64_t film_unit = mode_film_bytes(mode);
+    // Per-sample contribution film [chunk][P] bytes (unit) or [chunk][3][P]
+    // floats, at most film_budget_bytes (4 GiB) per chunk; chunks carry the
+    // running sum in acc.  (A chunk's work items are counted in 32 bits: at
+    // most 2^31 per chunk.)
     const uint64_t budget = cfg.film_budget_bytes;
-    // (a chunk's work items are counted in 32 bits: at most 2^31 per chunk)
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(
-        1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (12 * P)), 0x7fffffffull / P));
+        1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
     rs.paths_in_flight = (uint32_t)C;
-    spt_status st = ensure_workspace(sc->ws, K, Ck, cfg.plane_pad, (size_t)chunk * 3 * P + 3 * P, p.spp);
+    spt_status st = ensure_workspace(sc->ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P,
+                                     3 * P, (size_t)p.spp + kMaxDepthCasts);
     if (st) return st;
     Workspace& ws = sc->ws;
     // HIP events around the isect launches (the roofline kernel); every other
@@ -848,19 +868,28 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
     const bool timing_all = timing && (p.flags & SPT_FLAG_TIMING_ALL) != 0;
 
-    // PCG32 jump to each sample's first draw: s * (4 + 2D) (main.cpp:395,396,413).
+    // PCG32 jump to each sample's first draw, s * (4 + 2D), and from there to
+    // the bounce draw of each cast, 4 + 2 * cast (main.cpp:395,396,413).
     const uint64_t per_sample = 4ull + 2ull * p.max_depth;
     if (ws.jump_key_spp != p.spp || ws.jump_key_depth != p.max_depth) {
-        std::vector<PcgJump> jt(p.spp);
+        std::vector<PcgJump> jt((size_t)p.spp + p.max_depth);
         for (uint32_t s = 0; s < p.spp; s++) jt[s] = pcg_jump_coeffs((uint64_t)s * per_sample);
-        HIP_TRY(hipMemcpy(ws.jumps, jt.data(), sizeof(PcgJump) * p.spp, hipMemcpyHostToDevice));
+        for (uint32_t j = 0; j < p.max_depth; j++) jt[(size_t)p.spp + j] = pcg_jump_coeffs(4ull + 2ull * j);
+        HIP_TRY(hipMemcpy(ws.jumps, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
         ws.jump_key_spp = p.spp;
         ws.jump_key_depth = p.max_depth;
     }
 
     const Camera cam = make_camera(p);
-    float* sfilm = ws.film;
-    float* acc = ws.film + (size_t)chunk * 3 * P;
+    float* sfilm = (float*)ws.film;
+    uint8_t* sflag = (uint8_t*)ws.film;
+    float* acc = ws.acc;
+    const auto resolve = [&](uint32_t s0, uint32_t ns) {
+        return mode == kModeUnit
+                   ? launch_resolve_flags(sflag, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
+                                          p.env[0], p.env[1], p.env[2], stream)
+                   : launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp, stream);
+    };
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
     HIP_TRY(hipMemsetAsync(ws.stats, 0, sizeof(Stats), stream));
@@ -897,8 +926,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     PathQueue q[kMaxStreams][2];
     for (int k = 0; k < K; k++) {
         Sub& b = ws.sub[k];
-        q[k][0] = carve_queue(b.qa, queue_stride(b.cap, b.pad));
-        q[k][1] = carve_queue(b.qb, queue_stride(b.cap, b.pad));
+        q[k][0] = carve_queue(b.qa, queue_stride(b.cap, b.pad), mode_planes(mode));
+        q[k][1] = carve_queue(b.qb, queue_stride(b.cap, b.pad), mode_planes(mode));
         IsectQueueArgs& I = ia[k];
         I.sc = sc->dev();
         I.hits = (float4*)b.hits;
@@ -917,6 +946,10 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         S.sc = sc->dev();
         S.hits = (const float4*)b.hits;
         S.sfilm = sfilm;
+        S.sflag = sflag;
+        S.sample_jump = ws.jumps;
+        S.cast_jump = ws.jumps + p.spp;
+        S.initstate = p.rng_initstate;
         S.P = (uint32_t)P; S.W = p.width; S.max_depth = p.max_depth;
         S.xcd_remap = (cfg.xcd_remap >> 1) & 1u;
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
@@ -929,7 +962,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
         R.initstate = p.rng_initstate;
-        R.carry_l = sc->emission != nullptr;
+        R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
     }
 
@@ -940,6 +973,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.cam = cam;
         F.sample_jump = ws.jumps;
         F.sfilm = sfilm;
+        F.sflag = sflag;
         F.stats = ws.stats->stats;
         F.next = &ws.sub[0].cnt->isect_next;
         F.initstate = p.rng_initstate;
@@ -961,12 +995,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             F.count = (uint32_t)((uint64_t)ns * P);  // <= 4 GiB / 12 B per chunk
             F.sample0 = s0;
             HIP_TRY(hipMemsetAsync(F.next, 0, sizeof(uint32_t), stream));
-            if ((st = mark(1, stream, [&] { return launch_fused(F, stream, &lanes); }))) return st;
-            if ((st = mark(3, stream, [&] {
-                     return launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                           stream);
-                 })))
-                return st;
+            if ((st = mark(1, stream, [&] { return launch_fused(F, mode, stream, &lanes); }))) return st;
+            if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
             iters++;
         }
         C = lanes;
@@ -1045,7 +1075,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
                     sa[k].in = q[k][c]; sa[k].out = q[k][nx];
                     sa[k].count_in = &b.cnt->qn[c];
                     sa[k].count_out = &b.cnt->surv[nx];
-                    if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], known[k], strm[k]); }))) return st;
+                    if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], mode, known[k], strm[k]); }))) return st;
                     ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
                     ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
                     ra[k].surv_clear = &b.cnt->surv[c];
@@ -1097,11 +1127,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             HIP_TRY(hipEventRecord(ws.sub[k].join_ev, strm[k]));
             HIP_TRY(hipStreamWaitEvent(stream, ws.sub[k].join_ev, 0));
         }
-        if ((st = mark(3, stream, [&] {
-                 return launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                       stream);
-             })))
-            return st;
+        if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
     }
     unsigned long long hstats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIP_TRY(hipMemcpyAsync(hstats, ws.stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));

@@ -651,14 +651,25 @@ __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32
     d = camera_sample_dir(cam, x, y, o, xi_x, xi_y);
 }
 
-__device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix,
-                                           uint32_t meta, uint64_t rng, float tr, float tg, float tb, float lr,
-                                           float lg, float lb, bool with_l) {
-    q.q0[j] = make_float4(tr, tg, tb, u2f(pix));
+// A path's planes (PathQueue): the ray always, throughput / radiance as the mode needs.
+template <int kMode>
+__device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix, uint32_t meta,
+                                           float tr, float tg, float tb, float lr, float lg, float lb) {
     q.q1[j] = make_float4(o.x, o.y, o.z, u2f(meta));
-    q.q2[j] = make_float4(d.x, d.y, d.z, u2f((uint32_t)rng));
-    q.rng_hi[j] = (uint32_t)(rng >> 32);
-    if (with_l) q.rad[j] = make_float4(lr, lg, lb, 0.0f);  // only scenes with emitters
+    q.q2[j] = make_float4(d.x, d.y, d.z, u2f(pix));
+    if (kMode >= kModeAlbedo) q.q0[j] = make_float4(tr, tg, tb, 0.0f);
+    if (kMode == kModeEmit) q.rad[j] = make_float4(lr, lg, lb, 0.0f);
+}
+
+// PCG32 of global pixel gpix (main.cpp:376) advanced past the draws a path
+// has consumed: the sample's jump (s * (4 + 2D)) then the cast's (4 camera
+// draws + 2 per earlier cast, main.cpp:395,396,413).
+__device__ __forceinline__ Pcg32 path_rng(uint64_t initstate, uint32_t gpix, const PcgJump& js, const PcgJump& jc) {
+    Pcg32 r;
+    r.seed(initstate, (uint64_t)gpix);
+    r.state = pcg_apply(js, r.state, r.inc);
+    r.state = pcg_apply(jc, r.state, r.inc);
+    return r;
 }
 
 // Refill: start work items [cursor, cursor + total) in queue slots
@@ -666,6 +677,7 @@ __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o,
 // refill hands consecutive lanes consecutive pixels of one sample (coherent
 // camera rays).  RNG: the pixel's PCG32 stream (main.cpp:376) advanced to the
 // sample's first draw, s * (4 + 2D) draws (main.cpp:395,396,413 per sample).
+template <int kMode>
 __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     const uint32_t surv = *a.surv;
     const uint64_t cur = a.cursor_in ? *a.cursor_in : a.cursor_init;
@@ -697,20 +709,22 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     rng.state = pcg_apply(a.sample_jump[s], rng.state, rng.inc);
     V3 o, d;
     camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
-    store_path(a.q, surv + i, o, d, p, s << kMetaDepthBits, rng.state, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f,
-               0.0f, a.carry_l);  // main.cpp:391
+    store_path<kMode>(a.q, surv + i, o, d, p, s << kMetaDepthBits, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f, 0.0f);  // main.cpp:391
 }
 
 // ----------------------------------------------------------------- shade
 // main.cpp:404-425 for one cast of every queued path.  A path that ends
-// writes its gathered radiance (throughput x sky radiance on escape, plus
-// emitted radiance with emitters) to sfilm[sample][c][pixel]; survivors are
+// writes its contribution once per (sample, pixel): unit mode one byte
+// (escaped or not: the sky term is added in sample order by the resolve),
+// otherwise its gathered radiance (throughput x sky radiance on escape, plus
+// emitted radiance with emitters) to sfilm[sample][c][pixel].  Survivors are
 // compacted into the out queue with a wave ballot + mbcnt rank and one
 // atomicAdd per block.  Phase 1 decides which paths survive (miss, last cast,
 // albedo, roulette) from the hit and the material word alone, so the block's
-// queue atomic is issued before phase 2 (new ray: RNG draw, interpolated
-// normal, Frame3, cosine sample) and its latency hides behind that work.
-template <bool kEmit>
+// queue atomic is issued before phase 2 (new ray: RNG derivation and draw,
+// interpolated normal, Frame3, cosine sample) and its latency hides behind
+// that work.
+template <int kMode>
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
@@ -727,56 +741,60 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     float4 hit = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m0 = hit, m1 = hit, m2 = hit;
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
-    uint64_t rs = 0;
     if (i < n) {
-        const float4 q0 = a.in.q0[i], q1 = a.in.q1[i];
-        pix = f2u(q0.w);
+        const float4 q1 = a.in.q1[i], q2 = a.in.q2[i];
         meta = f2u(q1.w);
+        pix = f2u(q2.w);
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
         hit = a.hits[i];
         const int32_t slot = (int32_t)f2u(hit.x);
-        tr = q0.x; tg = q0.y; tb = q0.z;
-        if (kEmit) { const float4 l = a.in.rad[i]; lr = l.x; lg = l.y; lb = l.z; }
-        bool term = true;
+        if (kMode >= kModeAlbedo) { const float4 q0 = a.in.q0[i]; tr = q0.x; tg = q0.y; tb = q0.z; }
+        if (kMode == kModeEmit) { const float4 l = a.in.rad[i]; lr = l.x; lg = l.y; lb = l.z; }
+        bool term = true, escaped = false;
         if (slot < 0) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
-            lr = lr + tr * a.env_r;
-            lg = lg + tg * a.env_g;
-            lb = lb + tb * a.env_b;
+            escaped = true;
+            if (kMode != kModeUnit) {
+                lr = lr + tr * a.env_r;
+                lg = lg + tg * a.env_g;
+                lb = lb + tb * a.env_b;
+            }
         } else {
             const bool bounce = depth + 1 < a.max_depth;
-            m0 = a.sc.snrm[(size_t)slot * 3];  // n0 + material id
+            if (kMode == kModeEmit || bounce) m0 = a.sc.snrm[(size_t)slot * 3];  // n0 + material id
             if (bounce) {
                 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
                 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
-                const float4 q2 = a.in.q2[i];
-                rs = ((uint64_t)a.in.rng_hi[i] << 32) | f2u(q2.w);
                 o = v3(q1.x, q1.y, q1.z);
                 d = v3(q2.x, q2.y, q2.z);
-            }
-            uint32_t mat = f2u(m0.w);
-            if (kEmit && mat < a.sc.nemit) {
-                // emitted radiance at the hit (smallpt obj.e; not in the reference)
-                lr = lr + tr * a.sc.emission[mat * 3];
-                lg = lg + tg * a.sc.emission[mat * 3 + 1];
-                lb = lb + tb * a.sc.emission[mat * 3 + 2];
-            }
-            if (bounce) {
                 const uint32_t lx = pix % a.W, ly = pix / a.W;
                 gpix = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group) * a.W + lx;
-                if (mat >= a.sc.nmat) mat = 0;
-                tr = tr * a.sc.albedo[mat * 3];                  // main.cpp:422
-                tg = tg * a.sc.albedo[mat * 3 + 1];
-                tb = tb * a.sc.albedo[mat * 3 + 2];
-                term = false;
-                if (depth + 1 >= a.rr_start) {
-                    const float q = fmaxf(tr, fmaxf(tg, tb));
-                    if (q < 1.0f) {
-                        if (rr_uniform(gpix, sample, depth) >= q) {
-                            term = true;
-                        } else {
-                            tr = tr / q; tg = tg / q; tb = tb / q;
+            }
+            if (kMode == kModeUnit) {
+                term = !bounce;  // albedo 1: the throughput stays 1, roulette never fires
+            } else {
+                uint32_t mat = f2u(m0.w);
+                if (kMode == kModeEmit && mat < a.sc.nemit) {
+                    // emitted radiance at the hit (smallpt obj.e; not in the reference)
+                    lr = lr + tr * a.sc.emission[mat * 3];
+                    lg = lg + tg * a.sc.emission[mat * 3 + 1];
+                    lb = lb + tb * a.sc.emission[mat * 3 + 2];
+                }
+                if (bounce) {
+                    if (mat >= a.sc.nmat) mat = 0;
+                    tr = tr * a.sc.albedo[mat * 3];                  // main.cpp:422
+                    tg = tg * a.sc.albedo[mat * 3 + 1];
+                    tb = tb * a.sc.albedo[mat * 3 + 2];
+                    term = false;
+                    if (depth + 1 >= a.rr_start) {
+                        const float q = fmaxf(tr, fmaxf(tg, tb));
+                        if (q < 1.0f) {
+                            if (rr_uniform(gpix, sample, depth) >= q) {
+                                term = true;
+                            } else {
+                                tr = tr / q; tg = tg / q; tb = tb / q;
+                            }
                         }
                     }
                 }
@@ -785,10 +803,14 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
         emit = !term;
         if (term) {
-            float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
-            f[0] = lr;
-            f[(size_t)a.P] = lg;
-            f[(size_t)2 * a.P] = lb;
+            if (kMode == kModeUnit) {
+                a.sflag[(size_t)(sample - a.sample0) * a.P + pix] = escaped ? 1 : 0;
+            } else {
+                float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
+                f[0] = lr;
+                f[(size_t)a.P] = lg;
+                f[(size_t)2 * a.P] = lb;
+            }
         }
     }
 
@@ -814,11 +836,10 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 
     // ---- phase 2: the bounce ray of every survivor
     V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
-    uint64_t nrng = 0;
     if (emit) {
-        Pcg32 rng;
-        rng.state = rs;
-        rng.inc = ((uint64_t)gpix << 1u) | 1u;
+        const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
+        const uint32_t sample = meta >> kMetaDepthBits;
+        Pcg32 rng = path_rng(a.initstate, gpix, a.sample_jump[sample], a.cast_jump[depth]);
         const float t = hit.y, u = hit.z, v = hit.w;
         float xi_x, xi_y;
         draw2(rng, a.rng_order, xi_x, xi_y);                   // main.cpp:413
@@ -829,7 +850,6 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         no = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);   // optix_backend.h:469, main.cpp:423
         const Frame fr = frame_from_normal(sn);                  // main.cpp:414
         nd = to_world(fr, cosine_hemisphere(xi_x, xi_y));        // main.cpp:418-419, 424
-        nrng = rng.state;
     }
     if (tid == 0) {
         uint32_t off = base;
@@ -839,7 +859,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
     }
     __syncthreads();
-    if (emit) store_path(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, nrng, tr, tg, tb, lr, lg, lb, kEmit);
+    if (emit) store_path<kMode>(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, tr, tg, tb, lr, lg, lb);
 }
 
 // ------------------------------------------------------------ fused render
@@ -854,9 +874,10 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 #ifndef SPT_FUSED_WAVES
 #define SPT_FUSED_WAVES 5
 #endif
-template <typename Tr, bool kEmit>
+template <typename Tr, int kMode>
 __global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
+    constexpr bool kEmit = kMode == kModeEmit;
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
     const uint32_t n = a.count;
@@ -885,9 +906,11 @@ void render_fused_kernel(FusedArgs a) {
                 const TraceHit hh = tr.hit(a.sc, L);
                 const int32_t slot = hh.slot;
                 if (slot < 0) {
-                    lr = lr + thr * a.env_r;                       // main.cpp:407
-                    lg = lg + thg * a.env_g;
-                    lb = lb + thb * a.env_b;
+                    if (kMode != kModeUnit) {
+                        lr = lr + thr * a.env_r;                   // main.cpp:407
+                        lg = lg + thg * a.env_g;
+                        lb = lb + thb * a.env_b;
+                    }
                 } else {
                     const float4 m0 = a.sc.snrm[(size_t)slot * 3];
                     uint32_t mat = f2u(m0.w);
@@ -897,12 +920,14 @@ void render_fused_kernel(FusedArgs a) {
                         lb = lb + thb * a.sc.emission[mat * 3 + 2];
                     }
                     if (depth + 1 < a.max_depth) {
-                        if (mat >= a.sc.nmat) mat = 0;
-                        thr = thr * a.sc.albedo[mat * 3];            // main.cpp:422
-                        thg = thg * a.sc.albedo[mat * 3 + 1];
-                        thb = thb * a.sc.albedo[mat * 3 + 2];
+                        if (kMode != kModeUnit) {
+                            if (mat >= a.sc.nmat) mat = 0;
+                            thr = thr * a.sc.albedo[mat * 3];        // main.cpp:422
+                            thg = thg * a.sc.albedo[mat * 3 + 1];
+                            thb = thb * a.sc.albedo[mat * 3 + 2];
+                        }
                         term = false;
-                        if (depth + 1 >= a.rr_start) {
+                        if (kMode != kModeUnit && depth + 1 >= a.rr_start) {
                             const float q = fmaxf(thr, fmaxf(thg, thb));
                             if (q < 1.0f) {
                                 if (rr_uniform(gpix, sample, depth) >= q) {
@@ -938,10 +963,14 @@ void render_fused_kernel(FusedArgs a) {
                     }
                 }
                 if (term) {
-                    float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
-                    f[0] = lr;
-                    f[(size_t)a.P] = lg;
-                    f[(size_t)2 * a.P] = lb;
+                    if (kMode == kModeUnit) {
+                        a.sflag[(size_t)(sample - a.sample0) * a.P + pix] = slot < 0 ? 1 : 0;
+                    } else {
+                        float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
+                        f[0] = lr;
+                        f[(size_t)a.P] = lg;
+                        f[(size_t)2 * a.P] = lb;
+                    }
                 }
             }
             // ---- new camera paths in free lanes (refill_kernel)
@@ -1017,6 +1046,30 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
     for (uint32_t c = 0; c < 3; c++) {
         float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
         for (uint32_t s = 0; s < nsamples; s++) sum = sum + sfilm[((size_t)s * 3 + c) * P + p];
+        if (last_chunk)
+            out[(size_t)c * P + p] = sum / (float)spp;
+        else
+            acc[(size_t)c * P + p] = sum;
+    }
+}
+
+// Unit mode: every escaped sample adds the sky radiance once, in sample order
+// (film += select(!hit && active, 1 x env, 0), main.cpp:407): the same
+// sequence of fp32 additions as the reference (adding the 0 of a sample that
+// did not escape leaves the sum as it is), then film /= spp (main.cpp:429).
+__global__ __launch_bounds__(256) void resolve_flags_kernel(const uint8_t* __restrict__ sflag,
+                                                            float* __restrict__ acc, float* __restrict__ out,
+                                                            uint32_t P, uint32_t nsamples, uint32_t first_chunk,
+                                                            uint32_t last_chunk, uint32_t spp, float env_r,
+                                                            float env_g, float env_b) {
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < nsamples; s++) k += sflag[(size_t)s * P + p];
+    const float env[3] = {env_r, env_g, env_b};
+    for (uint32_t c = 0; c < 3; c++) {
+        float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
+        for (uint32_t j = 0; j < k; j++) sum = sum + env[c];
         if (last_chunk)
             out[(size_t)c * P + p] = sum / (float)spp;
         else
@@ -1144,16 +1197,16 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s) {
+hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
-    if (a.sc.emission)
-        hipLaunchKernelGGL(shade_kernel<true>, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
-    else
-        hipLaunchKernelGGL(shade_kernel<false>, dim3(blocks_for(grid_items, kShadeBlock)), dim3(kShadeBlock), 0, s, a);
+    const dim3 g(blocks_for(grid_items, kShadeBlock)), b(kShadeBlock);
+    if (mode == kModeEmit) hipLaunchKernelGGL(shade_kernel<kModeEmit>, g, b, 0, s, a);
+    else if (mode == kModeAlbedo) hipLaunchKernelGGL(shade_kernel<kModeAlbedo>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(shade_kernel<kModeUnit>, g, b, 0, s, a);
     return hipGetLastError();
 }
 
-template <typename Tr, bool kEmit>
+template <typename Tr, int kMode>
 static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out) {
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
@@ -1163,7 +1216,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
     (void)hipGetDevice(&dev);
     if (!cached || cached_lds != lds || cached_dev != dev) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_fused_kernel<Tr, kEmit>, kIsectBlock, lds) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_fused_kernel<Tr, kMode>, kIsectBlock, lds) !=
                 hipSuccess || per_cu <= 0)
             per_cu = 1;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -1175,20 +1228,26 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
     const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)cached * a.grid_q8) >> 8)) : cached;
     const uint32_t blocks = min(scaled, blocks_for(a.count > 0 ? a.count : 1, kIsectBlock));
     if (lanes_out) *lanes_out = blocks * kIsectBlock;
-    hipLaunchKernelGGL((render_fused_kernel<Tr, kEmit>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
+    hipLaunchKernelGGL((render_fused_kernel<Tr, kMode>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_fused(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out) {
-    if (a.sc.nodes8)
-        return a.sc.emission ? launch_fused_t<Tracer8F, true>(a, s, lanes_out)
-                             : launch_fused_t<Tracer8F, false>(a, s, lanes_out);
-    return a.sc.emission ? launch_fused_t<Tracer, true>(a, s, lanes_out)
-                         : launch_fused_t<Tracer, false>(a, s, lanes_out);
+hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out) {
+    if (a.sc.nodes8) {
+        if (mode == kModeEmit) return launch_fused_t<Tracer8F, kModeEmit>(a, s, lanes_out);
+        if (mode == kModeAlbedo) return launch_fused_t<Tracer8F, kModeAlbedo>(a, s, lanes_out);
+        return launch_fused_t<Tracer8F, kModeUnit>(a, s, lanes_out);
+    }
+    if (mode == kModeEmit) return launch_fused_t<Tracer, kModeEmit>(a, s, lanes_out);
+    if (mode == kModeAlbedo) return launch_fused_t<Tracer, kModeAlbedo>(a, s, lanes_out);
+    return launch_fused_t<Tracer, kModeUnit>(a, s, lanes_out);
 }
 
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s) {
-    hipLaunchKernelGGL(refill_kernel, dim3(blocks_for(grid_items > 0 ? grid_items : 1, 256)), dim3(256), 0, s, a);
+    const dim3 g(blocks_for(grid_items > 0 ? grid_items : 1, 256)), b(256);
+    if (a.mode == kModeEmit) hipLaunchKernelGGL(refill_kernel<kModeEmit>, g, b, 0, s, a);
+    else if (a.mode == kModeAlbedo) hipLaunchKernelGGL(refill_kernel<kModeAlbedo>, g, b, 0, s, a);
+    else hipLaunchKernelGGL(refill_kernel<kModeUnit>, g, b, 0, s, a);
     return hipGetLastError();
 }
 
@@ -1197,6 +1256,15 @@ hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(resolve_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sfilm, acc, out, P, nsamples,
                        first_chunk, last_chunk, spp);
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve_flags(const uint8_t* sflag, float* acc, float* out, uint32_t P, uint32_t nsamples,
+                                uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, float env_r, float env_g,
+                                float env_b, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    hipLaunchKernelGGL(resolve_flags_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sflag, acc, out, P, nsamples,
+                       first_chunk, last_chunk, spp, env_r, env_g, env_b);
     return hipGetLastError();
 }
 

@@ -19,18 +19,30 @@ constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
 constexpr uint32_t kIsectChunk = 128;       // dynamic-share queue indices a wave takes per atomic
 constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
 
+// Path modes: what a path carries besides its ray.  The scene decides
+// (spt_render): unit = every albedo 1 and no emitters, the reference's own
+// case (main.cpp:234,244) — the throughput is always 1, roulette
+// never fires, and a path's film contribution is "escaped or not".
+enum PathMode : int {
+    kModeUnit = 0,    // q1, q2                  (32 B / path); film: one byte per (sample, pixel)
+    kModeAlbedo = 1,  // + q0 throughput          (48 B / path); film: RGB floats per (sample, pixel)
+    kModeEmit = 2     // + rad gathered radiance  (64 B / path); film: RGB floats
+};
+SPT_HD uint32_t mode_planes(int mode) { return mode == kModeUnit ? 2u : mode == kModeAlbedo ? 3u : 4u; }
+SPT_HD uint32_t mode_film_bytes(int mode) { return mode == kModeUnit ? 1u : 12u; }
+
 // Path queue: planes of 16-B quads grouped by who reads them, so a kernel
 // moves a path in a few dwordx4 accesses (one coalesced 1-KB wave instruction
 // each) instead of one 4-B plane per field:
-//   q0 = (tr, tg, tb, pix)        throughput, tile-local pixel  [shade: every path]
-//   q1 = (o.x, o.y, o.z, meta)    origin, sample << 8 | cast    [isect; shade: every path]
-//   q2 = (d.x, d.y, d.z, rng.lo)  direction, PCG32 state lo     [isect; shade: bounces]
-//   rng_hi                        PCG32 state hi (inc = 2 * global_pixel + 1)
-//   rad = (lr, lg, lb, -)         radiance gathered so far (emitters only)
+//   q1 = (o.x, o.y, o.z, meta)    origin, sample << 8 | cast    [isect, shade]
+//   q2 = (d.x, d.y, d.z, pix)     direction, tile-local pixel   [isect, shade]
+//   q0 = (tr, tg, tb, -)          throughput                    [shade; albedo / emit modes]
+//   rad = (lr, lg, lb, -)         radiance gathered so far      [shade; emit mode]
+// The PCG32 state is not stored: (pixel, sample, cast) fix how many draws the
+// path has consumed, s * (4 + 2D) + 4 + 2 * cast (main.cpp:395,396,413), so
+// shade re-derives it with two jump-ahead applications.
 struct PathQueue {
-    float4 *q0, *q1, *q2;
-    uint32_t* rng_hi;
-    float4* rad;
+    float4 *q1, *q2, *q0, *rad;
 };
 
 // Geometry on device, leaf ("slot") order.
@@ -93,7 +105,11 @@ struct ShadeArgs {
     const float4* hits;
     const uint32_t* count_in;
     uint32_t* count_out;        // survivors appended here (zeroed before the launch)
-    float* sfilm;               // [spp_chunk][3][P]: one contribution per (sample, pixel)
+    float* sfilm;               // [spp_chunk][3][P]: one contribution per (sample, pixel) (albedo / emit)
+    uint8_t* sflag;             // [spp_chunk][P]: escaped or not per (sample, pixel) (unit mode)
+    const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
+    const PcgJump* cast_jump;   // [max_depth]: jump by 4 + 2 * cast draws
+    uint64_t initstate;
     uint32_t P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     float env_r, env_g, env_b;
@@ -120,7 +136,7 @@ struct RefillArgs {
     uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     uint64_t initstate;
-    bool carry_l;               // write the gathered-radiance planes (emitters present)
+    int mode;                   // PathMode: which planes a new path fills
 };
 
 // Fused persistent render (one launch per sample chunk): every lane owns a
@@ -130,7 +146,8 @@ struct FusedArgs {
     DeviceScene sc;
     Camera cam;
     const PcgJump* sample_jump;
-    float* sfilm;               // [spp_chunk][3][P]
+    float* sfilm;               // [spp_chunk][3][P] (albedo / emit)
+    uint8_t* sflag;             // [spp_chunk][P] (unit mode)
     unsigned long long* stats;  // casts, continuations, regenerations
     uint32_t* next;             // dynamic work counter (zeroed before the launch)
     uint64_t work0, initstate;
@@ -161,11 +178,15 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
-hipError_t launch_fused(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out);
-hipError_t launch_shade(const ShadeArgs& a, uint32_t grid_items, hipStream_t s);
+hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out);
+hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
                           uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, hipStream_t s);
+// unit mode: film = env added once per escaped sample, in sample order
+hipError_t launch_resolve_flags(const uint8_t* sflag, float* acc, float* out, uint32_t P, uint32_t nsamples,
+                                uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, float env_r, float env_g,
+                                float env_b, hipStream_t s);
 hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s);
 
 }  // namespace spt

@@ -226,22 +226,36 @@ def small():
 @pytest.mark.parametrize("pipeline", ["wavefront", "fused"])
 @pytest.mark.parametrize("streams", [1, 2, 4])
 @pytest.mark.parametrize("per_chunk", [1, 2, 3])
-def test_film_chunking_bitexact(small, pipeline, streams, per_chunk):
+@pytest.mark.parametrize("mode", ["unit", "albedo", "emit"])
+def test_film_chunking_bitexact(small, pipeline, streams, per_chunk, mode):
     """the sample-chunked path (per-sample film over budget; the
     running sum carried in acc across chunks) with 1-3 samples per chunk,
-    both pipelines, 1-4 streams, roulette on — bit-equal to the oracle."""
+    both pipelines, 1-4 streams, in every path mode: unit (the reference's
+    albedo 1: one escape byte per sample and pixel), albedo (roulette on) and
+    emitters (RGB floats) — bit-equal to the oracle."""
     m, albedo, osc = small
     w, h, spp, depth = 40, 30, 7, 5
+    film_unit = 1 if mode == "unit" else 12
     cfg = sptamd.default_config()
-    cfg.film_budget_bytes = 12 * w * h * per_chunk
+    cfg.film_budget_bytes = film_unit * w * h * per_chunk
     cfg.streams = streams
     s = sptamd.Scene(config=cfg)
     s.add_arrays(m)
     s.commit(0)
-    s.backend.set_albedo(albedo)
-    assert s.backend.config["film_budget_bytes"] == 12 * w * h * per_chunk
-    got, st = render(s, w, h, spp, depth, rr_start_depth=2, pipeline=pipeline, wavefront_paths=1500)
-    ref, casts = osc.render(O.reference_params(w, h, spp, depth, rr_start_depth=2))
+    kw = dict(rr_start_depth=2, env=(0.3, 0.7, 1.0))
+    if mode == "unit":
+        osc = O.OracleScene(m)
+    elif mode == "albedo":
+        s.backend.set_albedo(albedo)
+    else:
+        emi = np.zeros((len(albedo), 3), np.float32)
+        emi[1] = (1.5, 0.5, 0.25)
+        s.backend.set_albedo(albedo)
+        s.backend.set_emission(emi)
+        osc = O.OracleScene(m, albedo=albedo, emission=emi)
+    assert s.backend.config["film_budget_bytes"] == film_unit * w * h * per_chunk
+    got, st = render(s, w, h, spp, depth, pipeline=pipeline, wavefront_paths=1500, **kw)
+    ref, casts = osc.render(O.reference_params(w, h, spp, depth, **kw))
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts
     assert st["streams"] == (1 if pipeline == "fused" else streams)
