@@ -41,6 +41,9 @@ for s in "$@"; do
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmc|pmc1|pmc2|pmc3|pmc4) c=${s#pmc}; run $s 900 env CONFIG=${c:-1} bash tools/pmc_isect.sh gpurun_out/pmc ;;
+    pmcshade) run pmcshade 600 env KERNEL=shade_kernel bash tools/pmc_sweep.sh gpurun_out/pmc_shade "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" ;;
+    pmcshade1) run pmcshade1 600 env SPT_STREAMS=1 KERNEL=shade_kernel bash tools/pmc_sweep.sh gpurun_out/pmc_shade1 "FETCH_SIZE" "WRITE_SIZE" ;;
+    pmc1s) run pmc1s 900 env SPT_STREAMS=1 CONFIG=1 bash tools/pmc_isect.sh gpurun_out/pmc1s ;;
     prof1s) run prof1s 600 env SPT_STREAMS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1s -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
     tilesim) run tilesim 400 python tools/tile_sim.py ;;

@@ -1,7 +1,7 @@
 """Per-launch and per-cast PMC figures of isect_queue_kernel from rocprofv3
 --pmc passes over one bench config.
 
-    python tools/pmc_isect.py OUT_JSON KEY BENCH_LOG COUNTER_CSV [COUNTER_CSV ...]
+    python tools/pmc_isect.py OUT_JSON KEY BENCH_LOG COUNTER_CSV [COUNTER_CSV ...] [--kernel NAME]
 
 Each CSV is one pass (run_counter_collection.csv).  Every counter is averaged
 over the isect dispatches of its pass.  BENCH_LOG holds the bench JSON line of
@@ -44,12 +44,19 @@ def bench_line(log):
 
 
 def main(out, key, log, *paths):
-    per = passes(paths)
+    kernel = "isect_queue"
+    paths = list(paths)
+    if "--kernel" in paths:
+        i = paths.index("--kernel")
+        kernel = paths[i + 1]
+        del paths[i:i + 2]
+    per = passes(paths, kernel)
     mean = {c: sum(v.values()) / max(len(v), 1) for c, v in per.items()}
     b = bench_line(log)
     roof = b["roofline"]
+    # casts per launch: the isect launches and the shade launches both run once per cast
     casts = roof["algorithmic_bytes_per_launch"] / roof["bytes_per_unit"]
-    rec = {"kernel": "isect_queue_kernel", "workload": b["config"]["workload"], "streams": b["config"]["streams"],
+    rec = {"kernel": kernel, "workload": b["config"]["workload"], "streams": b["config"]["streams"],
            "casts_per_launch": casts, "dispatches": {c: len(v) for c, v in per.items()}, "per_launch": mean,
            "source": [os.path.relpath(p) for p in paths]}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
