@@ -241,6 +241,18 @@ spt_status spt_scene_set_albedo(spt_scene scene, const float* albedo_rgb, uint32
  * hit (it must know which surface it reached). */
 spt_status spt_scene_set_emission(spt_scene scene, const float* emission_rgb, uint32_t nmat);
 
+/* LambertBsdf's reflectance image for one material (ImageTexture,
+ * main.cpp:34-80; the reference only ever builds 1 x 1 images, main.cpp:40-44,
+ * and its loader is empty, :37-39): rgb = width x height interleaved RGB
+ * floats.  A bounce off the material multiplies the throughput by the
+ * bilinear, clamped lookup at the hit's interpolated texcoord (main.cpp:62-76,
+ * 109-117), including the reference's texel index y * height + x (main.cpp:52;
+ * it equals y * width + x for square images), kept inside the image.  Without
+ * texcoords the lookup is at (0, 0).  rgb NULL removes the image (the albedo
+ * table's constant applies again).  At most 2^26 texels per image. */
+spt_status spt_scene_set_texture(spt_scene scene, uint32_t material, const float* rgb, uint32_t width,
+                                 uint32_t height);
+
 spt_status spt_scene_get_stats(spt_scene scene, spt_scene_stats* out);
 
 /* The host builders alone, without a device (diagnostics; the host sanitizer

@@ -32,6 +32,10 @@
  *   ORACLE_ALT_TRI        Moller-Trumbore (not watertight) instead of the Woop
  *                         test standing in for OptiX's triangle test (optix_backend.h:314)
  *   (all)                 the four together
+ *   ORACLE_ALT_TEX1X1     (separately) every material's constant colour through
+ *                         ImageTexture::eval as the reference's 1x1 image
+ *                         (main.cpp:40-44, 62-76): bilinear weights that sum to
+ *                         1 only up to rounding, instead of the exact constant
  */
 #include "oracle.h"
 
@@ -257,6 +261,12 @@ typedef struct {
     int32_t nmat;
     float* emission; /* nemit * 3 or NULL */
     int32_t nemit;
+    float* tc;       /* ntri * 6: texcoords t0 t1 t2 (0 where missing) or NULL */
+    /* per-material reflectance images (LambertBsdf::m_reflectance, main.cpp:102-120):
+     * tex_w[m] = 0 -> the albedo table's constant */
+    int32_t ntex;
+    int32_t* tex_w; int32_t* tex_h;
+    float** tex_rgb; /* interleaved RGB, w * h texels */
     int32_t use_bvh;
     onode* nodes;
     int64_t nnodes;
@@ -451,11 +461,83 @@ void oracle_scene_set_emission(void* scene, const float* emission, int32_t nmat)
     s->nemit = nmat;
 }
 
+void oracle_scene_set_texcoords(void* scene, const int32_t* tc_tri, const float* tc, int64_t ntc) {
+    oscene* s = (oscene*)scene;
+    free(s->tc);
+    s->tc = NULL;
+    if (!tc_tri || !tc) return;
+    s->tc = (float*)malloc(sizeof(float) * 6 * (size_t)(s->ntri > 0 ? s->ntri : 1));
+    for (int64_t t = 0; t < s->ntri; t++)
+        for (int k = 0; k < 3; k++) {
+            int32_t i = tc_tri[t * 3 + k];
+            int ok = i >= 0 && i < ntc;
+            s->tc[t * 6 + k * 2] = ok ? tc[(int64_t)i * 2] : 0.0f;
+            s->tc[t * 6 + k * 2 + 1] = ok ? tc[(int64_t)i * 2 + 1] : 0.0f;
+        }
+}
+
+void oracle_scene_set_texture(void* scene, int32_t mat, const float* rgb, int32_t w, int32_t h) {
+    oscene* s = (oscene*)scene;
+    if (mat < 0) return;
+    if (mat >= s->ntex) {
+        int32_t n = mat + 1;
+        s->tex_w = (int32_t*)realloc(s->tex_w, sizeof(int32_t) * (size_t)n);
+        s->tex_h = (int32_t*)realloc(s->tex_h, sizeof(int32_t) * (size_t)n);
+        s->tex_rgb = (float**)realloc(s->tex_rgb, sizeof(float*) * (size_t)n);
+        for (int32_t i = s->ntex; i < n; i++) { s->tex_w[i] = 0; s->tex_h[i] = 0; s->tex_rgb[i] = NULL; }
+        s->ntex = n;
+    }
+    free(s->tex_rgb[mat]);
+    s->tex_rgb[mat] = NULL;
+    s->tex_w[mat] = 0;
+    s->tex_h[mat] = 0;
+    if (!rgb || w <= 0 || h <= 0) return;
+    s->tex_rgb[mat] = (float*)malloc(sizeof(float) * 3 * (size_t)w * (size_t)h);
+    memcpy(s->tex_rgb[mat], rgb, sizeof(float) * 3 * (size_t)w * (size_t)h);
+    s->tex_w[mat] = w;
+    s->tex_h[mat] = h;
+}
+
 void oracle_scene_destroy(void* scene) {
     oscene* s = (oscene*)scene;
     if (!s) return;
     free(s->v); free(s->n); free(s->mat); free(s->albedo); free(s->emission); free(s->nodes); free(s->prims);
+    free(s->tc);
+    for (int32_t i = 0; i < s->ntex; i++) free(s->tex_rgb[i]);
+    free(s->tex_w); free(s->tex_h); free(s->tex_rgb);
     free(s);
+}
+
+/* ImageTexture::texel_fetch_wrap / texel_fetch (main.cpp:47-60): clamp to the
+ * image, then the reference's index y * size.y + x (main.cpp:52; the row
+ * stride is the height, harmless for square images), kept inside the image
+ * (the reference would gather out of bounds when height > width). */
+static inline const float* texel(const float* img, int32_t w, int32_t h, int32_t x, int32_t y) {
+    x = x < 0 ? 0 : (x > w - 1 ? w - 1 : x);
+    y = y < 0 ? 0 : (y > h - 1 ? h - 1 : y);
+    int64_t idx = (int64_t)y * h + x;
+    if (idx > (int64_t)w * h - 1) idx = (int64_t)w * h - 1;
+    return img + idx * 3;
+}
+/* ImageTexture::eval (main.cpp:62-76): bilinear with clamp, in the
+ * reference's operation order; uv scaled by the size, minus half a texel;
+ * floor2int of a coordinate clamped to +-2^30 (NaN -> -2^30). */
+static inline void texture_eval(const float* img, int32_t w, int32_t h, float u, float v, float out[3]) {
+    float sx = u * (float)w - 0.5f, sy = v * (float)h - 0.5f;
+    sx = fminf(fmaxf(sx, -1073741824.0f), 1073741824.0f);
+    sy = fminf(fmaxf(sy, -1073741824.0f), 1073741824.0f);
+    int32_t x = (int32_t)floorf(sx), y = (int32_t)floorf(sy);
+    float dx1 = sx - (float)x, dy1 = sy - (float)y;
+    float dx2 = 1.0f - dx1, dy2 = 1.0f - dy1;
+    const float* f00 = texel(img, w, h, x, y);
+    const float* f01 = texel(img, w, h, x, y + 1);
+    const float* f10 = texel(img, w, h, x + 1, y);
+    const float* f11 = texel(img, w, h, x + 1, y + 1);
+    for (int c = 0; c < 3; c++)
+        out[c] = (((f00[c] * dx2) * dy2 + (f01[c] * dx2) * dy1) + (f10[c] * dx1) * dy2) + (f11[c] * dx1) * dy1;
+}
+void oracle_texture_eval(const float* rgb, int32_t w, int32_t h, float u, float v, float* out3) {
+    texture_eval(rgb, w, h, u, v, out3);
 }
 
 /* ------------------------------------------------------ triangle (Woop) */
@@ -738,8 +820,31 @@ static void render_pixel(void* c_, int64_t li) {
             v3 lo = cosine_hemisphere(xi_x, xi_y);                /* main.cpp:418, :109-117 */
             v3 out = to_world(&f, lo);                            /* main.cpp:419 */
             int32_t m = s->mat[h.id];
+            int32_t mt = m;
             if (m < 0 || m >= s->nmat) m = 0;
-            for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * s->albedo[m * 3 + k]; /* :422 */
+            float refl[3] = {s->albedo[m * 3], s->albedo[m * 3 + 1], s->albedo[m * 3 + 2]};
+#ifdef ORACLE_ALT_TEX1X1
+            int tex = 1;  /* every material is an ImageTexture: a 1x1 image of its colour (main.cpp:40-44) */
+            const float* timg = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_rgb[mt] : &s->albedo[m * 3];
+            int32_t tw = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_w[mt] : 1;
+            int32_t th = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_h[mt] : 1;
+#else
+            int tex = mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0;
+            const float* timg = tex ? s->tex_rgb[mt] : NULL;
+            int32_t tw = tex ? s->tex_w[mt] : 0, th = tex ? s->tex_h[mt] : 0;
+#endif
+            if (tex) {
+                /* LambertBsdf::sample -> m_reflectance->eval(texcoord) (main.cpp:109-117):
+                 * texcoord = barycentric_interpolate (optix_backend.h:395-401, add_math.h:4-7) */
+                float tu = 0.0f, tv = 0.0f;
+                if (s->tc) {
+                    const float* c = &s->tc[(int64_t)h.id * 6];
+                    tu = (w * c[0] + h.u * c[2]) + h.v * c[4];
+                    tv = (w * c[1] + h.u * c[3]) + h.v * c[5];
+                }
+                texture_eval(timg, tw, th, tu, tv, refl);
+            }
+            for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * refl[k];   /* :422 */
             o = hp;                                               /* main.cpp:423 */
             d = out;                                              /* main.cpp:424 */
             if (j + 1 >= p->rr_start_depth && j + 1 < p->max_depth) {

@@ -38,6 +38,12 @@ void* oracle_scene_create(const int32_t* pos_tri, const float* pos, int64_t nver
 void oracle_scene_destroy(void* scene);
 /* Per-material emission (nmat x 3), NULL/0 = none (see oracle_render). */
 void oracle_scene_set_emission(void* scene, const float* emission, int32_t nmat);
+/* Texcoord triplets + texcoords (main.cpp:141-251 layout); missing (-1) -> (0, 0). */
+void oracle_scene_set_texcoords(void* scene, const int32_t* tc_tri, const float* tc, int64_t ntc);
+/* Material mat's reflectance image (ImageTexture, main.cpp:34-80): interleaved RGB,
+ * w x h texels; rgb NULL removes it (the albedo constant applies). */
+void oracle_scene_set_texture(void* scene, int32_t mat, const float* rgb, int32_t w, int32_t h);
+void oracle_texture_eval(const float* rgb, int32_t w, int32_t h, float u, float v, float* out3);
 
 /* wavefront_isect.cu:80-112 semantics: masked lanes untouched; miss -> id -1. */
 void oracle_intersect(void* scene, const float* ox, const float* oy, const float* oz,

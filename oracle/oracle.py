@@ -32,7 +32,7 @@ def build() -> str:
 
 
 # oracle.c header: one unpinned arithmetic choice each, and all four at once
-VARIANTS = ("sincos", "rsqrt", "fma", "tri", "all")
+VARIANTS = ("sincos", "rsqrt", "fma", "tri", "all", "tex1x1")
 
 
 def _load(path=LIB_PATH):
@@ -44,6 +44,9 @@ def _load(path=LIB_PATH):
     lib.oracle_scene_create.argtypes = [vp, vp, c_int64, c_int64, vp, vp, c_int64, vp, vp, c_int32, c_int32]
     lib.oracle_scene_destroy.argtypes = [vp]
     lib.oracle_scene_set_emission.argtypes = [vp, vp, c_int32]
+    lib.oracle_scene_set_texcoords.argtypes = [vp, vp, vp, c_int64]
+    lib.oracle_scene_set_texture.argtypes = [vp, c_int32, vp, c_int32, c_int32]
+    lib.oracle_texture_eval.argtypes = [vp, c_int32, c_int32, c_float, c_float, vp]
     lib.oracle_intersect.argtypes = [vp] + [vp] * 8 + [vp, c_uint32] + [vp] * 4 + [c_int64, c_int32, c_int32]
     lib.oracle_render.restype = c_int32
     lib.oracle_render.argtypes = [vp, POINTER(OracleParams), vp, c_int32, vp, c_int32, POINTER(c_uint64)]
@@ -99,7 +102,8 @@ def reference_params(width=512, height=512, spp=100, max_depth=2, camera=None, r
 
 
 class OracleScene:
-    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None, lib=None):
+    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None, lib=None, textures=None):
+        """textures: {material id: (H, W, 3) float32 image} (ImageTexture, main.cpp:34-80)."""
         self.lib = lib if lib is not None else globals()["lib"]
         lib = self.lib
         self.pt = np.ascontiguousarray(mesh["pos_tri"], dtype=np.int32)
@@ -118,6 +122,15 @@ class OracleScene:
         self.emi = None if emi is None else np.ascontiguousarray(emi, dtype=np.float32).reshape(-1, 3)
         if self.emi is not None:
             lib.oracle_scene_set_emission(self.h, _p(self.emi), self.emi.shape[0])
+        if mesh.get("tc_tri") is not None and mesh.get("tc") is not None:
+            self.tt = np.ascontiguousarray(mesh["tc_tri"], dtype=np.int32)
+            self.tc = np.ascontiguousarray(mesh["tc"], dtype=np.float32)
+            lib.oracle_scene_set_texcoords(self.h, _p(self.tt), _p(self.tc), self.tc.size // 2)
+        self.tex = {}
+        for mat, img in (textures or {}).items():
+            img = np.ascontiguousarray(img, dtype=np.float32)
+            self.tex[mat] = img
+            lib.oracle_scene_set_texture(self.h, int(mat), _p(img), img.shape[1], img.shape[0])
 
     def __del__(self):
         if getattr(self, "h", None) and getattr(self, "lib", None) is not None:  # (module teardown at exit)
@@ -151,6 +164,14 @@ class OracleScene:
         if rc != 0:
             raise RuntimeError(f"oracle_render failed: {rc}")
         return film, int(casts.value)
+
+
+def texture_eval(img, u: float, v: float) -> np.ndarray:
+    """ImageTexture::eval (main.cpp:62-76) of an (H, W, 3) image at (u, v)."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros(3, np.float32)
+    lib.oracle_texture_eval(_p(img), img.shape[1], img.shape[0], u, v, _p(out))
+    return out
 
 
 def pcg32_seq(initstate: int, initseq: int, n: int) -> np.ndarray:

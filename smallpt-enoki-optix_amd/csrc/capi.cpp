@@ -150,6 +150,13 @@ struct spt_scene_t {
     float* emission = nullptr;
     uint32_t nemit = 0;
     bool albedo_unit = true;  // every albedo entry is exactly 1 (the reference's case)
+    // per-material reflectance images (spt_scene_set_texture): host copies and
+    // the device arrays rebuilt from them
+    std::vector<std::vector<float4>> tex_img;
+    std::vector<uint32_t> tex_w, tex_h;
+    uint4* tex_info = nullptr;
+    float4* texels = nullptr;
+    uint32_t ntex = 0;      // entries of tex_info (0: no images)
     uint32_t stack_depth = 1;
     spt_scene_stats stats{};
     Workspace ws;
@@ -158,11 +165,13 @@ struct spt_scene_t {
         DeviceScene d;
         d.nodes = nodes; d.nodes8 = nodes8; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
         d.albedo = albedo; d.nmat = nmat; d.emission = emission; d.nemit = nemit; d.stack_depth = stack_depth; d.empty = ntri == 0;
+        d.tex_info = tex_info; d.ntex = ntex; d.texels = texels;
         return d;
     }
     void release() {
         ws.release();
         hfree(nodes); hfree(nodes8); hfree(emission); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
+        hfree(tex_info); hfree(texels);
     }
 };
 
@@ -687,6 +696,49 @@ spt_status spt_scene_get_config(spt_scene sc, spt_config* out) {
     return SPT_OK;
 }
 
+spt_status spt_scene_set_texture(spt_scene sc, uint32_t material, const float* rgb, uint32_t width, uint32_t height) {
+    if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_texture: NULL scene");
+    if (rgb && (width == 0 || height == 0)) return fail(SPT_ERR_INVALID, "spt_scene_set_texture: empty image");
+    if (rgb && (uint64_t)width * height > (1ull << 26))
+        return fail(SPT_ERR_LIMIT, "spt_scene_set_texture: %u x %u texels exceeds 2^26", width, height);
+    if (material >= (1u << 20)) return fail(SPT_ERR_LIMIT, "spt_scene_set_texture: material %u >= 2^20", material);
+    std::lock_guard<std::mutex> lk(sc->mu);
+    if (material >= sc->tex_img.size()) {
+        sc->tex_img.resize(material + 1);
+        sc->tex_w.resize(material + 1, 0);
+        sc->tex_h.resize(material + 1, 0);
+    }
+    std::vector<float4>& img = sc->tex_img[material];
+    img.clear();
+    sc->tex_w[material] = sc->tex_h[material] = 0;
+    if (rgb) {
+        img.resize((size_t)width * height);
+        for (size_t i = 0; i < img.size(); i++) img[i] = make_float4(rgb[i * 3], rgb[i * 3 + 1], rgb[i * 3 + 2], 0.0f);
+        sc->tex_w[material] = width;
+        sc->tex_h[material] = height;
+    }
+    // rebuild the device arrays: one texel array, one (first, w, h, has) entry per material
+    std::vector<uint4> info(sc->tex_img.size());
+    std::vector<float4> all;
+    uint32_t used = 0;
+    for (size_t m = 0; m < sc->tex_img.size(); m++) {
+        const bool has = !sc->tex_img[m].empty();
+        info[m] = make_uint4((uint32_t)all.size(), sc->tex_w[m], sc->tex_h[m], has ? 1u : 0u);
+        all.insert(all.end(), sc->tex_img[m].begin(), sc->tex_img[m].end());
+        if (has) used = (uint32_t)m + 1;
+    }
+    hfree(sc->tex_info);
+    hfree(sc->texels);
+    sc->ntex = 0;
+    if (used) {
+        spt_status us = upload(&sc->tex_info, info.data(), sizeof(uint4) * used);
+        if (!us) us = upload(&sc->texels, all.data(), sizeof(float4) * all.size());
+        if (us) return us;
+        sc->ntex = used;
+    }
+    return SPT_OK;
+}
+
 spt_status spt_scene_get_stats(spt_scene sc, spt_scene_stats* out) {
     if (!sc || !out) return fail(SPT_ERR_INVALID, "spt_scene_get_stats: NULL argument");
     *out = sc->stats;
@@ -849,7 +901,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const uint64_t Ck = (C + K - 1) / K;
     // What a path carries (spt_internal.h PathMode): the reference's case
     // (every albedo 1, no emitters) needs only the ray and an escaped flag.
-    const int mode = sc->emission ? kModeEmit : (sc->albedo_unit ? kModeUnit : kModeAlbedo);
+    const int mode = sc->emission ? kModeEmit : (sc->albedo_unit && sc->ntex == 0 ? kModeUnit : kModeAlbedo);
     const uint64_t film_unit = mode_film_bytes(mode);
     // Per-sample contribution film [chunk][P] bytes (unit) or [chunk][3][P]
     // floats, at most film_budget_bytes (4 GiB) per chunk; chunks carry the

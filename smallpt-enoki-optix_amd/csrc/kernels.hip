@@ -782,10 +782,10 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
                     lb = lb + tb * a.sc.emission[mat * 3 + 2];
                 }
                 if (bounce) {
-                    if (mat >= a.sc.nmat) mat = 0;
-                    tr = tr * a.sc.albedo[mat * 3];                  // main.cpp:422
-                    tg = tg * a.sc.albedo[mat * 3 + 1];
-                    tb = tb * a.sc.albedo[mat * 3 + 2];
+                    const V3 rf = reflectance(a.sc, mat, (uint32_t)slot, hit.z, hit.w);  // main.cpp:418
+                    tr = tr * rf.x;                                  // main.cpp:422
+                    tg = tg * rf.y;
+                    tb = tb * rf.z;
                     term = false;
                     if (depth + 1 >= a.rr_start) {
                         const float q = fmaxf(tr, fmaxf(tg, tb));
@@ -921,10 +921,10 @@ void render_fused_kernel(FusedArgs a) {
                     }
                     if (depth + 1 < a.max_depth) {
                         if (kMode != kModeUnit) {
-                            if (mat >= a.sc.nmat) mat = 0;
-                            thr = thr * a.sc.albedo[mat * 3];        // main.cpp:422
-                            thg = thg * a.sc.albedo[mat * 3 + 1];
-                            thb = thb * a.sc.albedo[mat * 3 + 2];
+                            const V3 rf = reflectance(a.sc, mat, (uint32_t)slot, hh.u, hh.v);  // main.cpp:418
+                            thr = thr * rf.x;                        // main.cpp:422
+                            thg = thg * rf.y;
+                            thb = thb * rf.z;
                         }
                         term = false;
                         if (kMode != kModeUnit && depth + 1 >= a.rr_start) {

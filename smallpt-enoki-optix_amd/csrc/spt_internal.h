@@ -59,7 +59,55 @@ struct DeviceScene {
     uint32_t nemit;
     uint32_t stack_depth;  // LDS stack entries per lane (one word each)
     uint32_t empty;        // no triangles
+    const uint4* tex_info; // per material: first texel, width, height, 1 if it has an image (null: none)
+    uint32_t ntex;         // entries of tex_info
+    const float4* texels;  // RGB(-) texels of every image
 };
+
+// ImageTexture::texel_fetch_wrap / texel_fetch (main.cpp:47-60): clamp, then
+// the reference's index y * size.y + x (main.cpp:52), kept inside the image.
+SPT_HD float4 texel_fetch(const float4* img, uint32_t w, uint32_t h, int32_t x, int32_t y) {
+    x = x < 0 ? 0 : (x > (int32_t)w - 1 ? (int32_t)w - 1 : x);
+    y = y < 0 ? 0 : (y > (int32_t)h - 1 ? (int32_t)h - 1 : y);
+    uint64_t idx = (uint64_t)y * h + (uint64_t)x;
+    const uint64_t last = (uint64_t)w * h - 1;
+    return img[idx > last ? last : idx];
+}
+// ImageTexture::eval (main.cpp:62-76): bilinear with clamp in the reference's
+// operation order; the scaled coordinate is clamped to +-2^30 before
+// floor2int (NaN -> -2^30), the oracle does the same.
+SPT_HD V3 texture_eval(const float4* img, uint32_t w, uint32_t h, float u, float v) {
+    float sx = u * (float)w - 0.5f, sy = v * (float)h - 0.5f;
+    sx = fminf(fmaxf(sx, -1073741824.0f), 1073741824.0f);
+    sy = fminf(fmaxf(sy, -1073741824.0f), 1073741824.0f);
+    const int32_t x = (int32_t)floorf(sx), y = (int32_t)floorf(sy);
+    const float dx1 = sx - (float)x, dy1 = sy - (float)y;
+    const float dx2 = 1.0f - dx1, dy2 = 1.0f - dy1;
+    const float4 f00 = texel_fetch(img, w, h, x, y), f01 = texel_fetch(img, w, h, x, y + 1);
+    const float4 f10 = texel_fetch(img, w, h, x + 1, y), f11 = texel_fetch(img, w, h, x + 1, y + 1);
+    return v3((((f00.x * dx2) * dy2 + (f01.x * dx2) * dy1) + (f10.x * dx1) * dy2) + (f11.x * dx1) * dy1,
+              (((f00.y * dx2) * dy2 + (f01.y * dx2) * dy1) + (f10.y * dx1) * dy2) + (f11.y * dx1) * dy1,
+              (((f00.z * dx2) * dy2 + (f01.z * dx2) * dy1) + (f10.z * dx1) * dy2) + (f11.z * dx1) * dy1);
+}
+
+// LambertBsdf::sample's contribution (main.cpp:109-117, 422): the material's
+// image at the hit's texcoord, else its albedo constant (material ids outside
+// the table use material 0).
+SPT_HD V3 reflectance(const DeviceScene& sc, uint32_t mat, uint32_t slot, float u, float v) {
+    if (mat < sc.ntex && sc.tex_info[mat].w) {
+        const uint4 ti = sc.tex_info[mat];
+        float tu = 0.0f, tv = 0.0f;
+        if (sc.tc) {  // barycentric_interpolate (add_math.h:4-7, optix_backend.h:395-401)
+            const float* c = sc.tc + (size_t)slot * 6;
+            const float w = (1.0f - u) - v;
+            tu = (w * c[0] + u * c[2]) + v * c[4];
+            tv = (w * c[1] + u * c[3]) + v * c[5];
+        }
+        return texture_eval(sc.texels + ti.x, ti.y, ti.z, tu, tv);
+    }
+    if (mat >= sc.nmat) mat = 0;
+    return v3(sc.albedo[mat * 3], sc.albedo[mat * 3 + 1], sc.albedo[mat * 3 + 2]);
+}
 
 struct IsectQueueArgs {
     DeviceScene sc;

@@ -144,6 +144,17 @@ class HipBackend:
         e = np.ascontiguousarray(np.asarray(emission_rgb, dtype=np.float32).reshape(-1, 3))
         check(lib.spt_scene_set_emission(self._scene, e.ctypes.data, e.shape[0]), "spt_scene_set_emission")
 
+    def set_texture(self, material: int, image=None) -> None:
+        """Material `material`'s reflectance image (ImageTexture, main.cpp:34-80):
+        (H, W, 3) float32, or None to remove it."""
+        if image is None:
+            check(lib.spt_scene_set_texture(self._scene, material, None, 0, 0), "spt_scene_set_texture")
+            return
+        img = np.ascontiguousarray(np.asarray(image, dtype=np.float32))
+        assert img.ndim == 3 and img.shape[2] == 3, "texture must be (H, W, 3)"
+        check(lib.spt_scene_set_texture(self._scene, material, img.ctypes.data, img.shape[1], img.shape[0]),
+              "spt_scene_set_texture")
+
     @property
     def handle(self):
         return self._scene

@@ -277,6 +277,25 @@ def city_camera() -> dict:
                 focal_dist=1.0, fov_y=0.9, film_size_y=0.035)
 
 
+def with_planar_uv(mesh: Dict[str, np.ndarray], scale: float = 0.3, offset=(0.5, 0.5)) -> Dict[str, np.ndarray]:
+    """A copy of mesh with per-vertex texcoords from a planar projection
+    (u = x * scale + offset, v = z * scale + offset), tc_tri = pos_tri — for
+    the textured-material tests (the generated stand-ins carry no vt)."""
+    m = dict(mesh)
+    p = np.asarray(mesh["pos"], np.float32)
+    m["tc"] = np.stack([p[:, 0] * np.float32(scale) + np.float32(offset[0]),
+                        p[:, 2] * np.float32(scale) + np.float32(offset[1])], 1).astype(np.float32)
+    m["tc_tri"] = np.asarray(mesh["pos_tri"], np.int32).copy()
+    return m
+
+
+def checker(w: int, h: int, a=(0.9, 0.8, 0.2), b=(0.2, 0.4, 0.9), cell: int = 1) -> np.ndarray:
+    """(h, w, 3) float32 checkerboard image."""
+    y, x = np.mgrid[0:h, 0:w]
+    sel = ((x // cell + y // cell) % 2 == 0)[..., None]
+    return np.where(sel, np.float32(a), np.float32(b)).astype(np.float32)
+
+
 def write_obj(path: str, mesh: Dict[str, np.ndarray], mtl: str = None) -> None:
     """Write mesh as OBJ (+ .mtl) using v / vn / f v//vn and usemtl groups."""
     mtl = mtl or os.path.splitext(path)[0] + ".mtl"

@@ -294,3 +294,47 @@ def test_bvh_ties_and_parallel_rays_equal_bruteforce():
     for x, y in zip(bvh, brute):
         np.testing.assert_array_equal(x, y)
     assert (brute[0] >= 0).mean() > 0.95
+
+
+def test_texture_eval_known_answers():
+    """ImageTexture::eval (main.cpp:62-76): texel centres return the texel, the
+    edges clamp, the index is y * height + x (main.cpp:52), and a 1 x 1 image
+    is its colour up to the rounding of the bilinear weights."""
+    img = np.arange(2 * 2 * 3, dtype=np.float32).reshape(2, 2, 3)
+    for (x, y) in ((0, 0), (1, 0), (0, 1), (1, 1)):
+        np.testing.assert_array_equal(O.texture_eval(img, (x + 0.5) / 2, (y + 0.5) / 2), img[y, x])
+    np.testing.assert_array_equal(O.texture_eval(img, -3.0, -3.0), img[0, 0])      # clamped
+    np.testing.assert_array_equal(O.texture_eval(img, 7.0, 7.0), img[1, 1])
+    mid = O.texture_eval(img, 0.5, 0.5)                                                 # bilinear centre
+    np.testing.assert_allclose(mid, img.reshape(4, 3).mean(0), rtol=1e-6)
+    # non-square: 4 wide, 2 high -> texel (x, y) read from flat index y * 2 + x
+    wide = np.arange(2 * 4 * 3, dtype=np.float32).reshape(2, 4, 3)
+    flat = wide.reshape(-1, 3)
+    np.testing.assert_array_equal(O.texture_eval(wide, 3.5 / 4, 1.5 / 2), flat[1 * 2 + 3])
+    # 2 wide, 4 high: y * 4 + x past the end is kept inside the image (last texel)
+    tall = np.arange(4 * 2 * 3, dtype=np.float32).reshape(4, 2, 3)
+    np.testing.assert_array_equal(O.texture_eval(tall, 1.5 / 2, 3.5 / 4), tall.reshape(-1, 3)[-1])
+    one = np.full((1, 1, 3), 0.7, np.float32)
+    rng = np.random.default_rng(0)
+    vals = np.array([O.texture_eval(one, *rng.uniform(-2, 2, 2)) for _ in range(500)])
+    assert np.all(np.abs(vals - np.float32(0.7)) <= 2 * np.spacing(np.float32(0.7)))
+    assert np.any(vals != np.float32(0.7))     # the reference's weights do not always sum to exactly 1
+
+
+def test_tex1x1_variant_within_tolerance():
+    """The albedo table stands in for the reference's 1 x 1 ImageTexture of each
+    material's colour (main.cpp:40-44); evaluated as the reference does, the
+    bilinear weights differ from 1 by rounding only — inside §8c's tolerance."""
+    from test_parity_tolerance import assert_within_tolerance
+    m = scenes.with_planar_uv(scenes.mitsuba_synth(detail=0.25))
+    p = O.reference_params(128, 128, 32, 6)
+    base, _ = O.OracleScene(m).render(p)
+    alt, _ = O.OracleScene(m, lib=O.variant("tex1x1")).render(p)
+    assert_within_tolerance(alt, base, 32, "tex1x1")
+    # at 32 spp the 1-ulp weight sums vanish in the film sum; one sample per
+    # pixel shows them (the variant is live: texcoords vary)
+    p1 = O.reference_params(128, 128, 1, 3)
+    one, _ = O.OracleScene(m).render(p1)
+    one_alt, _ = O.OracleScene(m, lib=O.variant("tex1x1")).render(p1)
+    assert not np.array_equal(one_alt, one)
+    np.testing.assert_allclose(one_alt, one, rtol=1e-6, atol=0)
