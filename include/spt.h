@@ -241,6 +241,26 @@ spt_status spt_scene_set_albedo(spt_scene scene, const float* albedo_rgb, uint32
  * hit (it must know which surface it reached). */
 spt_status spt_scene_set_emission(spt_scene scene, const float* emission_rgb, uint32_t nmat);
 
+/* smallpt's scene primitives and materials (the reference renders triangle
+ * meshes with Lambert BSDFs only; BASELINE config 2 is smallpt's Cornell box).
+ *
+ * spt_scene_set_spheres: n analytic spheres, center_radius = n x (cx, cy, cz,
+ * r) floats, mat_id = n material ids (NULL: material 0), tested against every
+ * ray after the triangle BVH (a list: smallpt-sized sets, n <= 256).  A sphere
+ * hit reports tri_id = -2 - k in spt_intersect (k = the sphere's index).
+ * NULL / n = 0 removes them.
+ *
+ * spt_scene_set_material_kinds: per material SPT_MAT_DIFFUSE (Lambert with
+ * the reference's un-normalised, unflipped shading normal on triangles, the
+ * outward normal flipped toward the ray on spheres — smallpt's nl),
+ * SPT_MAT_MIRROR (smallpt SPEC: ideal reflection) or SPT_MAT_GLASS (smallpt
+ * REFR: index 1.5, Schlick Fresnel, reflect with probability P = 1/4 + Re/2
+ * chosen by the bounce draw's first number, weight Re/P or (1-Re)/(1-P)).
+ * Albedo (and textures) multiply every kind.  Default: all diffuse. */
+enum { SPT_MAT_DIFFUSE = 0, SPT_MAT_MIRROR = 1, SPT_MAT_GLASS = 2 };
+spt_status spt_scene_set_spheres(spt_scene scene, const float* center_radius, const int32_t* mat_id, uint32_t n);
+spt_status spt_scene_set_material_kinds(spt_scene scene, const uint32_t* kinds, uint32_t nmat);
+
 /* LambertBsdf's reflectance image for one material (ImageTexture,
  * main.cpp:34-80; the reference only ever builds 1 x 1 images, main.cpp:40-44,
  * and its loader is empty, :37-39): rgb = width x height interleaved RGB

@@ -267,6 +267,9 @@ typedef struct {
     int32_t ntex;
     int32_t* tex_w; int32_t* tex_h;
     float** tex_rgb; /* interleaved RGB, w * h texels */
+    /* smallpt's analytic spheres (cx, cy, cz, r) + material, after the BVH */
+    float* sph; int32_t* sph_mat; int32_t nsph;
+    uint32_t* kind; int32_t nkind;  /* SPT_MAT_*: 0 diffuse, 1 mirror, 2 glass */
     int32_t use_bvh;
     onode* nodes;
     int64_t nnodes;
@@ -498,11 +501,33 @@ void oracle_scene_set_texture(void* scene, int32_t mat, const float* rgb, int32_
     s->tex_h[mat] = h;
 }
 
+void oracle_scene_set_spheres(void* scene, const float* cr, const int32_t* mat, int32_t n) {
+    oscene* s = (oscene*)scene;
+    free(s->sph); free(s->sph_mat);
+    s->sph = NULL; s->sph_mat = NULL; s->nsph = 0;
+    if (!cr || n <= 0) return;
+    s->sph = (float*)malloc(sizeof(float) * 4 * (size_t)n);
+    s->sph_mat = (int32_t*)malloc(sizeof(int32_t) * (size_t)n);
+    memcpy(s->sph, cr, sizeof(float) * 4 * (size_t)n);
+    for (int32_t k = 0; k < n; k++) s->sph_mat[k] = mat ? mat[k] : 0;
+    s->nsph = n;
+}
+
+void oracle_scene_set_material_kinds(void* scene, const uint32_t* kinds, int32_t n) {
+    oscene* s = (oscene*)scene;
+    free(s->kind);
+    s->kind = NULL; s->nkind = 0;
+    if (!kinds || n <= 0) return;
+    s->kind = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)n);
+    memcpy(s->kind, kinds, sizeof(uint32_t) * (size_t)n);
+    s->nkind = n;
+}
+
 void oracle_scene_destroy(void* scene) {
     oscene* s = (oscene*)scene;
     if (!s) return;
     free(s->v); free(s->n); free(s->mat); free(s->albedo); free(s->emission); free(s->nodes); free(s->prims);
-    free(s->tc);
+    free(s->tc); free(s->sph); free(s->sph_mat); free(s->kind);
     for (int32_t i = 0; i < s->ntex; i++) free(s->tex_rgb[i]);
     free(s->tex_w); free(s->tex_h); free(s->tex_rgb);
     free(s);
@@ -717,6 +742,36 @@ typedef struct {
     int32_t* id; float *t, *u, *v;
     int closest;
 } isect_ctx;
+/* ------------------------------------------------- smallpt spheres, kinds */
+/* smallpt's Sphere::intersect in the ray's own t units: the nearer root in
+ * [tmin, tmax], else +inf (op relative to the centre; same order as the GPU). */
+static inline float sphere_t(v3 o, v3 d, const float* sp, float tmin, float tmax) {
+    v3 op = mk(sp[0] - o.x, sp[1] - o.y, sp[2] - o.z);
+    float a = dot3(d, d);
+    float b = dot3(op, d);
+    float c = dot3(op, op) - sp[3] * sp[3];
+    float det = b * b - a * c;
+    if (!(det >= 0.0f)) return INFINITY;
+    float sq = sqrtf(det);
+    float t0 = (b - sq) / a, t1 = (b + sq) / a;
+    if (t0 >= tmin && t0 <= tmax) return t0;
+    if (t1 >= tmin && t1 <= tmax) return t1;
+    return INFINITY;
+}
+/* The spheres after the BVH: a sphere nearer than the current hit wins (ties
+ * keep the triangle); id = -2 - k.  Any-hit: the first sphere hit, only when
+ * no triangle was hit. */
+static inline void trace_spheres(const oscene* s, v3 o, v3 d, float tmin, int anyhit, ohit* h) {
+    if (anyhit && h->id != -1) return;
+    for (int32_t k = 0; k < s->nsph; k++) {
+        float t = sphere_t(o, d, &s->sph[k * 4], tmin, h->t);
+        if (t < h->t) {
+            h->t = t; h->id = -2 - k; h->u = 0.0f; h->v = 0.0f;
+            if (anyhit) return;
+        }
+    }
+}
+
 static void isect_one(void* c_, int64_t i) {
     isect_ctx* c = (isect_ctx*)c_;
     uint8_t m = (c->mask_size == 1) ? c->mask[0] : c->mask[i];  /* wavefront_isect.cu:86 */
@@ -727,8 +782,10 @@ static void isect_one(void* c_, int64_t i) {
     wray_setup(&r);
     ohit h;
     trace(c->s, &r, c->tmin[i], c->tmax[i], c->closest, &h);
+    if (c->s->nsph) trace_spheres(c->s, mk(r.o[0], r.o[1], r.o[2]), mk(r.d[0], r.d[1], r.d[2]), c->tmin[i],
+                                  !c->closest, &h);
     c->id[i] = h.id;                                             /* -1 on miss (wavefront_isect.cu:70) */
-    if (h.id >= 0) { c->t[i] = h.t; c->u[i] = h.u; c->v[i] = h.v; }
+    if (h.id != -1) { c->t[i] = h.t; c->u[i] = h.u; c->v[i] = h.v; }
 }
 void oracle_intersect(void* scene, const float* ox, const float* oy, const float* oz,
                       const float* dx, const float* dy, const float* dz,
@@ -738,6 +795,54 @@ void oracle_intersect(void* scene, const float* ox, const float* oy, const float
     isect_ctx c = {(const oscene*)scene, ox, oy, oz, dx, dy, dz, tmin, tmax, mask, mask_size,
                    tri_id, t, u, v, do_closest};
     parallel_for(n, 256, nthreads, isect_one, &c);
+}
+
+static inline uint32_t material_kind(const oscene* s, int32_t mat) {
+    return (s->kind && mat >= 0 && mat < s->nkind) ? s->kind[mat] : 0u;
+}
+/* Bounce direction and weight: triangles + diffuse = the reference's Lambert
+ * bounce (Frame3 of the un-normalised shading normal); spheres and the mirror /
+ * glass kinds = smallpt's radiance(): unit normal, flipped toward the ray for
+ * diffuse; SPEC reflects; REFR: index 1.5, Schlick, reflect with probability
+ * P = 1/4 + Re/2 by xi_x (weight Re/P, else Tr/(1-P)); TIR reflects. */
+static v3 scatter(const oscene* s, uint32_t kind, int32_t id, v3 d, v3 p, v3 sn, float xi_x, float xi_y,
+                  float* weight) {
+    *weight = 1.0f;
+    v3 n;
+    if (id >= 0) {
+        if (kind == 0) { frame3 f = frame_from_normal(sn); return to_world(&f, cosine_hemisphere(xi_x, xi_y)); }
+        n = normalize3(sn);
+    } else {
+        const float* sp = &s->sph[(-2 - id) * 4];
+        n = normalize3(mk(p.x - sp[0], p.y - sp[1], p.z - sp[2]));
+        if (kind == 0) {
+            v3 nl = dot3(n, d) < 0.0f ? n : mk(-n.x, -n.y, -n.z);
+            frame3 f = frame_from_normal(nl);
+            return to_world(&f, cosine_hemisphere(xi_x, xi_y));
+        }
+    }
+    v3 dn = normalize3(d);
+    float ndd = dot3(n, dn);
+    float k2 = 2.0f * ndd;
+    v3 refl = mk(dn.x - n.x * k2, dn.y - n.y * k2, dn.z - n.z * k2);
+    if (kind != 2) return refl;
+    int into = ndd < 0.0f;
+    v3 nl = into ? n : mk(-n.x, -n.y, -n.z);
+    float nc = 1.0f, nt = 1.5f;
+    float nnt = into ? nc / nt : nt / nc;
+    float ddn = dot3(dn, nl);
+    float cos2t = 1.0f - (nnt * nnt) * (1.0f - ddn * ddn);
+    if (cos2t < 0.0f) return refl;
+    float ks = (into ? 1.0f : -1.0f) * (ddn * nnt + sqrtf(cos2t));
+    v3 tdir = normalize3(mk(dn.x * nnt - n.x * ks, dn.y * nnt - n.y * ks, dn.z * nnt - n.z * ks));
+    float ea = nt - nc, eb = nt + nc;
+    float R0 = (ea * ea) / (eb * eb);
+    float c = 1.0f - (into ? -ddn : dot3(tdir, n));
+    float Re = R0 + (1.0f - R0) * ((((c * c) * c) * c) * c);
+    float Tr = 1.0f - Re, P = 0.25f + 0.5f * Re;
+    if (xi_x < P) { *weight = Re / P; return refl; }
+    *weight = Tr / (1.0f - P);
+    return tdir;
 }
 
 /* --------------------------------------------------------------- render */
@@ -795,31 +900,42 @@ static void render_pixel(void* c_, int64_t li) {
                 r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z;
                 wray_setup(&r);
                 trace(s, &r, 0.001f, 1e20f, 1, &h);               /* ray.h:15-17 */
+                if (s->nsph) trace_spheres(s, o, d, 0.001f, 0, &h);   /* smallpt's spheres */
                 casts++;
-                if (h.id < 0) {                                   /* main.cpp:407 */
+                if (h.id == -1) {                                 /* main.cpp:407 */
                     for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * p->env[k];
                 } else if (s->emission) {
                     /* emitted radiance at every hit (smallpt's obj.e; the
                      * reference has no emitters — SURVEY §8f row 3) */
-                    int32_t me = s->mat[h.id];
+                    int32_t me = h.id >= 0 ? s->mat[h.id] : s->sph_mat[-2 - h.id];
                     if (me >= 0 && me < s->nemit)
                         for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * s->emission[me * 3 + k];
                 }
             }
-            active = active && (h.id >= 0);                       /* main.cpp:410 */
+            active = active && (h.id != -1);                      /* main.cpp:410 */
             draw2(&rng, p->rng_order, &xi_x, &xi_y);              /* main.cpp:413 (always drawn) */
             if (!active) continue;
             /* optix_backend.h:469 (position), :483-484 (interpolated shading normal) */
-            const float* nv = &s->n[(int64_t)h.id * 9];
+            const int sph = h.id < -1;
             float w = (1.0f - h.u) - h.v;
-            v3 n = mk((w * nv[0] + h.u * nv[3]) + h.v * nv[6],
-                      (w * nv[1] + h.u * nv[4]) + h.v * nv[7],
-                      (w * nv[2] + h.u * nv[5]) + h.v * nv[8]);
+            v3 n = mk(0.0f, 0.0f, 0.0f);
+            if (!sph) {
+                const float* nv = &s->n[(int64_t)h.id * 9];
+                n = mk((w * nv[0] + h.u * nv[3]) + h.v * nv[6],
+                       (w * nv[1] + h.u * nv[4]) + h.v * nv[7],
+                       (w * nv[2] + h.u * nv[5]) + h.v * nv[8]);
+            }
             v3 hp = mk(o.x + h.t * d.x, o.y + h.t * d.y, o.z + h.t * d.z);
-            frame3 f = frame_from_normal(n);                      /* main.cpp:414 */
-            v3 lo = cosine_hemisphere(xi_x, xi_y);                /* main.cpp:418, :109-117 */
-            v3 out = to_world(&f, lo);                            /* main.cpp:419 */
-            int32_t m = s->mat[h.id];
+            int32_t m = sph ? s->sph_mat[-2 - h.id] : s->mat[h.id];
+            float sw = 1.0f;   /* the scatter weight (glass), applied after roulette */
+            v3 out;
+            if (!s->nsph && !s->nkind) {
+                frame3 f = frame_from_normal(n);                  /* main.cpp:414 */
+                v3 lo = cosine_hemisphere(xi_x, xi_y);            /* main.cpp:418, :109-117 */
+                out = to_world(&f, lo);                           /* main.cpp:419 */
+            } else {
+                out = scatter(s, material_kind(s, m), h.id, d, hp, n, xi_x, xi_y, &sw);
+            }
             int32_t mt = m;
             if (m < 0 || m >= s->nmat) m = 0;
             float refl[3] = {s->albedo[m * 3], s->albedo[m * 3 + 1], s->albedo[m * 3 + 2]};
@@ -837,7 +953,7 @@ static void render_pixel(void* c_, int64_t li) {
                 /* LambertBsdf::sample -> m_reflectance->eval(texcoord) (main.cpp:109-117):
                  * texcoord = barycentric_interpolate (optix_backend.h:395-401, add_math.h:4-7) */
                 float tu = 0.0f, tv = 0.0f;
-                if (s->tc) {
+                if (s->tc && !sph) {
                     const float* c = &s->tc[(int64_t)h.id * 6];
                     tu = (w * c[0] + h.u * c[2]) + h.v * c[4];
                     tv = (w * c[1] + h.u * c[3]) + h.v * c[5];
@@ -854,6 +970,7 @@ static void render_pixel(void* c_, int64_t li) {
                     for (int k = 0; k < 3; k++) contrib[k] = contrib[k] / q;
                 }
             }
+            for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * sw;  /* smallpt's glass weight */
         }
         /* Without emitters L is 0 or contrib * env: the same film sum as the
          * reference's per-miss film += contrib (main.cpp:407). */

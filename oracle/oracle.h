@@ -43,6 +43,11 @@ void oracle_scene_set_texcoords(void* scene, const int32_t* tc_tri, const float*
 /* Material mat's reflectance image (ImageTexture, main.cpp:34-80): interleaved RGB,
  * w x h texels; rgb NULL removes it (the albedo constant applies). */
 void oracle_scene_set_texture(void* scene, int32_t mat, const float* rgb, int32_t w, int32_t h);
+/* smallpt's analytic spheres: n x (cx, cy, cz, r) and a material per sphere,
+ * tested after the triangles (id -2 - k); kinds: SPT_MAT_* per material
+ * (0 diffuse, 1 mirror, 2 glass). */
+void oracle_scene_set_spheres(void* scene, const float* center_radius, const int32_t* mat, int32_t n);
+void oracle_scene_set_material_kinds(void* scene, const uint32_t* kinds, int32_t n);
 void oracle_texture_eval(const float* rgb, int32_t w, int32_t h, float u, float v, float* out3);
 
 /* wavefront_isect.cu:80-112 semantics: masked lanes untouched; miss -> id -1. */

@@ -46,6 +46,8 @@ def _load(path=LIB_PATH):
     lib.oracle_scene_set_emission.argtypes = [vp, vp, c_int32]
     lib.oracle_scene_set_texcoords.argtypes = [vp, vp, vp, c_int64]
     lib.oracle_scene_set_texture.argtypes = [vp, c_int32, vp, c_int32, c_int32]
+    lib.oracle_scene_set_spheres.argtypes = [vp, vp, vp, c_int32]
+    lib.oracle_scene_set_material_kinds.argtypes = [vp, vp, c_int32]
     lib.oracle_texture_eval.argtypes = [vp, c_int32, c_int32, c_float, c_float, vp]
     lib.oracle_intersect.argtypes = [vp] + [vp] * 8 + [vp, c_uint32] + [vp] * 4 + [c_int64, c_int32, c_int32]
     lib.oracle_render.restype = c_int32
@@ -102,8 +104,13 @@ def reference_params(width=512, height=512, spp=100, max_depth=2, camera=None, r
 
 
 class OracleScene:
-    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None, lib=None, textures=None):
-        """textures: {material id: (H, W, 3) float32 image} (ImageTexture, main.cpp:34-80)."""
+    def __init__(self, mesh: dict, use_bvh: bool = True, albedo=None, emission=None, lib=None, textures=None,
+                 spheres=None, sphere_mat=None, kinds=None):
+        """textures: {material id: (H, W, 3) float32 image} (ImageTexture, main.cpp:34-80).
+        spheres: (n, 4) float32 (cx, cy, cz, r) with sphere_mat (n,) material ids —
+        smallpt's analytic spheres after the triangles; kinds: per-material
+        SPT_MAT_* (0 diffuse, 1 mirror, 2 glass).  Defaults come from the mesh
+        dict's "spheres" / "sphere_mat" / "kinds" keys."""
         self.lib = lib if lib is not None else globals()["lib"]
         lib = self.lib
         self.pt = np.ascontiguousarray(mesh["pos_tri"], dtype=np.int32)
@@ -126,6 +133,17 @@ class OracleScene:
             self.tt = np.ascontiguousarray(mesh["tc_tri"], dtype=np.int32)
             self.tc = np.ascontiguousarray(mesh["tc"], dtype=np.float32)
             lib.oracle_scene_set_texcoords(self.h, _p(self.tt), _p(self.tc), self.tc.size // 2)
+        sph = spheres if spheres is not None else mesh.get("spheres")
+        if sph is not None and len(sph):
+            self.sph = np.ascontiguousarray(sph, dtype=np.float32).reshape(-1, 4)
+            sm = sphere_mat if sphere_mat is not None else mesh.get("sphere_mat")
+            self.sph_mat = (np.zeros(self.sph.shape[0], np.int32) if sm is None
+                            else np.ascontiguousarray(sm, dtype=np.int32).reshape(-1))
+            lib.oracle_scene_set_spheres(self.h, _p(self.sph), _p(self.sph_mat), self.sph.shape[0])
+        kd = kinds if kinds is not None else mesh.get("kinds")
+        if kd is not None and len(kd):
+            self.kinds = np.ascontiguousarray(kd, dtype=np.uint32).reshape(-1)
+            lib.oracle_scene_set_material_kinds(self.h, _p(self.kinds), self.kinds.size)
         self.tex = {}
         for mat, img in (textures or {}).items():
             img = np.ascontiguousarray(img, dtype=np.float32)

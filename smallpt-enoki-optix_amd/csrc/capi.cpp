@@ -157,6 +157,11 @@ struct spt_scene_t {
     uint4* tex_info = nullptr;
     float4* texels = nullptr;
     uint32_t ntex = 0;      // entries of tex_info (0: no images)
+    float4* spheres = nullptr;   // smallpt's analytic spheres (spt_scene_set_spheres)
+    int32_t* sph_mat = nullptr;
+    uint32_t nsph = 0;
+    uint32_t* mat_kind = nullptr;  // SPT_MAT_* per material (spt_scene_set_material_kinds)
+    uint32_t nkind = 0;
     uint32_t stack_depth = 1;
     spt_scene_stats stats{};
     Workspace ws;
@@ -166,12 +171,14 @@ struct spt_scene_t {
         d.nodes = nodes; d.nodes8 = nodes8; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
         d.albedo = albedo; d.nmat = nmat; d.emission = emission; d.nemit = nemit; d.stack_depth = stack_depth; d.empty = ntri == 0;
         d.tex_info = tex_info; d.ntex = ntex; d.texels = texels;
+        d.spheres = spheres; d.sph_mat = sph_mat; d.nsph = nsph;
+        d.mat_kind = mat_kind; d.nkind = nkind;
         return d;
     }
     void release() {
         ws.release();
         hfree(nodes); hfree(nodes8); hfree(emission); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
-        hfree(tex_info); hfree(texels);
+        hfree(tex_info); hfree(texels); hfree(spheres); hfree(sph_mat); hfree(mat_kind);
     }
 };
 
@@ -739,6 +746,47 @@ spt_status spt_scene_set_texture(spt_scene sc, uint32_t material, const float* r
     return SPT_OK;
 }
 
+spt_status spt_scene_set_spheres(spt_scene sc, const float* center_radius, const int32_t* mat_id, uint32_t n) {
+    if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: NULL scene");
+    if (n > 256) return fail(SPT_ERR_LIMIT, "spt_scene_set_spheres: %u spheres (at most 256)", n);
+    if (n && !center_radius) return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: NULL spheres");
+    for (uint32_t k = 0; k < n; k++) {
+        const float* c = center_radius + (size_t)k * 4;
+        if (!std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]))
+            return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: sphere %u centre must be finite", k);
+        if (!(c[3] > 0.0f) || !std::isfinite(c[3]))
+            return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: sphere %u radius must be finite and > 0", k);
+    }
+    std::lock_guard<std::mutex> lk(sc->mu);
+    hfree(sc->spheres);
+    hfree(sc->sph_mat);
+    sc->nsph = 0;
+    if (!n) return SPT_OK;
+    std::vector<int32_t> mats(n, 0);
+    if (mat_id) std::memcpy(mats.data(), mat_id, sizeof(int32_t) * n);
+    spt_status us = upload(&sc->spheres, center_radius, sizeof(float4) * n);
+    if (!us) us = upload(&sc->sph_mat, mats.data(), sizeof(int32_t) * n);
+    if (us) return us;
+    sc->nsph = n;
+    return SPT_OK;
+}
+
+spt_status spt_scene_set_material_kinds(spt_scene sc, const uint32_t* kinds, uint32_t nmat) {
+    if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_material_kinds: NULL scene");
+    for (uint32_t i = 0; kinds && i < nmat; i++)
+        if (kinds[i] > SPT_MAT_GLASS) return fail(SPT_ERR_INVALID, "spt_scene_set_material_kinds: kind %u of material %u", kinds[i], i);
+    std::lock_guard<std::mutex> lk(sc->mu);
+    hfree(sc->mat_kind);
+    sc->nkind = 0;
+    bool any = false;
+    for (uint32_t i = 0; kinds && i < nmat; i++) any = any || kinds[i] != SPT_MAT_DIFFUSE;
+    if (!any) return SPT_OK;  // all diffuse: the default
+    spt_status us = upload(&sc->mat_kind, kinds, sizeof(uint32_t) * nmat);
+    if (us) return us;
+    sc->nkind = nmat;
+    return SPT_OK;
+}
+
 spt_status spt_scene_get_stats(spt_scene sc, spt_scene_stats* out) {
     if (!sc || !out) return fail(SPT_ERR_INVALID, "spt_scene_get_stats: NULL argument");
     *out = sc->stats;
@@ -818,7 +866,7 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL ray plane (needed for the position)");
     if (mask && mask_size != 1 && mask_size != n)
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: mask_size %u must be 1 or n=%u", mask_size, n);
-    if (sc->ntri == 0) return SPT_OK;
+    if (sc->ntri == 0 && sc->nsph == 0) return SPT_OK;
     HitInfoArgs a;
     a.sc = sc->dev();
     a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
@@ -830,6 +878,7 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
     a.snx = out->snx; a.sny = out->sny; a.snz = out->snz;
     a.tcu = out->tcu; a.tcv = out->tcv;
     a.mat_id = out->mat_id;
+    a.ntri = sc->ntri;
     HIP_TRY(launch_hit_info(a, (hipStream_t)stream));
     return SPT_OK;
 }
@@ -901,7 +950,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const uint64_t Ck = (C + K - 1) / K;
     // What a path carries (spt_internal.h PathMode): the reference's case
     // (every albedo 1, no emitters) needs only the ray and an escaped flag.
-    const int mode = sc->emission ? kModeEmit : (sc->albedo_unit && sc->ntex == 0 ? kModeUnit : kModeAlbedo);
+    const bool unit = sc->albedo_unit && sc->ntex == 0 && sc->nsph == 0 && sc->nkind == 0;
+    const int mode = sc->emission ? kModeEmit : (unit ? kModeUnit : kModeAlbedo);
     const uint64_t film_unit = mode_film_bytes(mode);
     // Per-sample contribution film [chunk][P] bytes (unit) or [chunk][3][P]
     // floats, at most film_budget_bytes (4 GiB) per chunk; chunks carry the

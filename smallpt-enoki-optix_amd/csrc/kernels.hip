@@ -43,6 +43,25 @@ struct TraceHit {
     float t, u, v;
 };
 
+// Analytic spheres after the BVH (smallpt's primitives, spt_scene_set_spheres):
+// a sphere nearer than the current hit wins (ties keep it); slot = -2 - k.
+// Any-hit queries stop at the first hit.
+__device__ __forceinline__ void trace_spheres(const DeviceScene& sc, V3 o, V3 d, float tmin, bool anyhit,
+                                              TraceHit& h) {
+    if (anyhit && h.slot != -1) return;
+    for (uint32_t k = 0; k < sc.nsph; k++) {
+        const float t = sphere_t(o, d, sc.spheres[k], tmin, h.t);
+        if (t < h.t) {
+            h.t = t;
+            h.slot = -2 - (int32_t)k;
+            h.id = 0xffffffffu;
+            h.u = 0.0f;
+            h.v = 0.0f;
+            if (anyhit) return;
+        }
+    }
+}
+
 struct NoStats {
     __device__ void node() {}
     __device__ void tri() {}
@@ -570,14 +589,15 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     const V3 d = v3(a.dx[i], a.dy[i], a.dz[i]);
     const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
     NoStats st;
-    const TraceHit h = a.sc.nodes8
-                           ? trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
-                           : trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
-    if (h.slot < 0) {
+    TraceHit h = a.sc.nodes8
+                     ? trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
+                     : trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
+    if (a.sc.nsph) trace_spheres(a.sc, o, d, tmin, a.closest == 0, h);
+    if (h.slot == -1) {
         a.tri_id[i] = -1;
         return;
     }
-    a.tri_id[i] = (int32_t)h.id;
+    a.tri_id[i] = h.slot >= 0 ? (int32_t)h.id : h.slot;  // spheres: -2 - k
     a.t[i] = h.t;
     a.u[i] = h.u;
     a.v[i] = h.v;
@@ -618,7 +638,18 @@ void isect_public_persistent_kernel(IsectPublicArgs a) {
                         const float tmin = a.tmin ? a.tmin[ray] : kRayTmin, tmax = a.tmax ? a.tmax[ray] : kRayTmax;
                         tr.init(a.sc, o, d, tmin, tmax, a.closest == 0, L);
                         busy = !tr.finished();
-                        if (!busy) a.tri_id[ray] = -1;  // empty scene
+                        if (!busy) {  // empty triangle set: the spheres alone
+                            TraceHit h = tr.hit(a.sc, L);
+                            if (a.sc.nsph) trace_spheres(a.sc, o, d, tmin, a.closest == 0, h);
+                            if (h.slot == -1) {
+                                a.tri_id[ray] = -1;
+                            } else {
+                                a.tri_id[ray] = h.slot;
+                                a.t[ray] = h.t;
+                                a.u[ray] = h.u;
+                                a.v[ray] = h.v;
+                            }
+                        }
                     }
                 }
                 pool += take;
@@ -627,11 +658,16 @@ void isect_public_persistent_kernel(IsectPublicArgs a) {
         }
         if (!__ballot(busy)) break;
         if (busy && tr.step(a.sc, L, st)) {
-            const TraceHit h = tr.hit(a.sc, L);
-            if (h.slot < 0) {
+            TraceHit h = tr.hit(a.sc, L);
+            if (a.sc.nsph) {
+                const float tmin = a.tmin ? a.tmin[ray] : kRayTmin;
+                trace_spheres(a.sc, v3(a.ox[ray], a.oy[ray], a.oz[ray]), v3(a.dx[ray], a.dy[ray], a.dz[ray]), tmin,
+                              a.closest == 0, h);
+            }
+            if (h.slot == -1) {
                 a.tri_id[ray] = -1;
             } else {
-                a.tri_id[ray] = (int32_t)h.id;
+                a.tri_id[ray] = h.slot >= 0 ? (int32_t)h.id : h.slot;
                 a.t[ray] = h.t;
                 a.u[ray] = h.u;
                 a.v[ray] = h.v;
@@ -724,7 +760,9 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 // queue atomic is issued before phase 2 (new ray: RNG derivation and draw,
 // interpolated normal, Frame3, cosine sample) and its latency hides behind
 // that work.
-template <int kMode>
+// kSpt: the scene has smallpt spheres or mirror / glass materials (a separate
+// instance, so plain scenes keep the leaner register budget).
+template <int kMode, bool kSpt>
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
@@ -737,7 +775,8 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 
     // ---- phase 1: survive or terminate (the bounce inputs load alongside)
     bool emit = false;
-    uint32_t pix = 0, meta = 0, gpix = 0;
+    uint32_t pix = 0, meta = 0, gpix = 0, kind = kMatDiffuse;
+    int32_t slot = -1;
     float4 hit = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m0 = hit, m1 = hit, m2 = hit;
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
@@ -748,11 +787,21 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
         hit = a.hits[i];
-        const int32_t slot = (int32_t)f2u(hit.x);
+        slot = (int32_t)f2u(hit.x);
+        if (kSpt && a.sc.nsph) {
+            // smallpt's analytic spheres after the triangle BVH (the isect kernel
+            // traces triangles only); a miss record carries t = tmax
+            TraceHit h;
+            h.slot = slot; h.id = 0u; h.t = hit.y; h.u = hit.z; h.v = hit.w;
+            trace_spheres(a.sc, v3(q1.x, q1.y, q1.z), v3(q2.x, q2.y, q2.z), kRayTmin,
+                          depth + 1 >= a.max_depth && !a.sc.emission, h);
+            slot = h.slot;
+            hit = make_float4(u2f((uint32_t)slot), h.t, h.u, h.v);
+        }
         if (kMode >= kModeAlbedo) { const float4 q0 = a.in.q0[i]; tr = q0.x; tg = q0.y; tb = q0.z; }
         if (kMode == kModeEmit) { const float4 l = a.in.rad[i]; lr = l.x; lg = l.y; lb = l.z; }
         bool term = true, escaped = false;
-        if (slot < 0) {
+        if (slot == -1) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
             escaped = true;
             if (kMode != kModeUnit) {
@@ -762,10 +811,13 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             }
         } else {
             const bool bounce = depth + 1 < a.max_depth;
-            if (kMode == kModeEmit || bounce) m0 = a.sc.snrm[(size_t)slot * 3];  // n0 + material id
+            const bool sph = kSpt && slot < -1;
+            if (!sph && (kMode == kModeEmit || bounce)) m0 = a.sc.snrm[(size_t)slot * 3];  // n0 + material id
             if (bounce) {
-                m1 = a.sc.snrm[(size_t)slot * 3 + 1];
-                m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+                if (!sph) {
+                    m1 = a.sc.snrm[(size_t)slot * 3 + 1];
+                    m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+                }
                 o = v3(q1.x, q1.y, q1.z);
                 d = v3(q2.x, q2.y, q2.z);
                 const uint32_t lx = pix % a.W, ly = pix / a.W;
@@ -774,7 +826,8 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             if (kMode == kModeUnit) {
                 term = !bounce;  // albedo 1: the throughput stays 1, roulette never fires
             } else {
-                uint32_t mat = f2u(m0.w);
+                uint32_t mat = sph ? (a.sc.sph_mat ? (uint32_t)a.sc.sph_mat[-2 - slot] : 0u) : f2u(m0.w);
+                if (kSpt) kind = material_kind(a.sc, mat);
                 if (kMode == kModeEmit && mat < a.sc.nemit) {
                     // emitted radiance at the hit (smallpt obj.e; not in the reference)
                     lr = lr + tr * a.sc.emission[mat * 3];
@@ -848,8 +901,15 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
                          (w * m0.y + u * m1.y) + v * m2.y,
                          (w * m0.z + u * m1.z) + v * m2.z);
         no = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);   // optix_backend.h:469, main.cpp:423
-        const Frame fr = frame_from_normal(sn);                  // main.cpp:414
-        nd = to_world(fr, cosine_hemisphere(xi_x, xi_y));        // main.cpp:418-419, 424
+        if (!kSpt) {
+            const Frame fr = frame_from_normal(sn);              // main.cpp:414
+            nd = to_world(fr, cosine_hemisphere(xi_x, xi_y));    // main.cpp:418-419, 424
+        } else {
+            // Lambert on triangles as above; spheres / mirror / glass as smallpt
+            float wgt;
+            nd = scatter(a.sc, kind, slot, d, no, sn, xi_x, xi_y, wgt);
+            tr = tr * wgt; tg = tg * wgt; tb = tb * wgt;
+        }
     }
     if (tid == 0) {
         uint32_t off = base;
@@ -903,17 +963,20 @@ void render_fused_kernel(FusedArgs a) {
                 pending = false;
                 casts++;
                 bool term = true;
-                const TraceHit hh = tr.hit(a.sc, L);
+                TraceHit hh = tr.hit(a.sc, L);
+                if (kMode != kModeUnit && a.sc.nsph)  // smallpt's spheres after the BVH
+                    trace_spheres(a.sc, tr.o, dir, kRayTmin, depth + 1 >= a.max_depth && !kEmit, hh);
                 const int32_t slot = hh.slot;
-                if (slot < 0) {
+                const bool sph = kMode != kModeUnit && slot < -1;
+                if (slot == -1) {
                     if (kMode != kModeUnit) {
                         lr = lr + thr * a.env_r;                   // main.cpp:407
                         lg = lg + thg * a.env_g;
                         lb = lb + thb * a.env_b;
                     }
                 } else {
-                    const float4 m0 = a.sc.snrm[(size_t)slot * 3];
-                    uint32_t mat = f2u(m0.w);
+                    const float4 m0 = sph ? make_float4(0.0f, 0.0f, 0.0f, 0.0f) : a.sc.snrm[(size_t)slot * 3];
+                    uint32_t mat = sph ? (a.sc.sph_mat ? (uint32_t)a.sc.sph_mat[-2 - slot] : 0u) : f2u(m0.w);
                     if (kEmit && mat < a.sc.nemit) {
                         lr = lr + thr * a.sc.emission[mat * 3];
                         lg = lg + thg * a.sc.emission[mat * 3 + 1];
@@ -938,8 +1001,9 @@ void render_fused_kernel(FusedArgs a) {
                             }
                         }
                         if (!term) {
-                            const float4 m1 = a.sc.snrm[(size_t)slot * 3 + 1];
-                            const float4 m2 = a.sc.snrm[(size_t)slot * 3 + 2];
+                            const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                            const float4 m1 = sph ? zero : a.sc.snrm[(size_t)slot * 3 + 1];
+                            const float4 m2 = sph ? zero : a.sc.snrm[(size_t)slot * 3 + 2];
                             Pcg32 rng;
                             rng.state = rs;
                             rng.inc = ((uint64_t)gpix << 1u) | 1u;
@@ -952,8 +1016,14 @@ void render_fused_kernel(FusedArgs a) {
                                              (w * m0.z + u * m1.z) + v * m2.z);
                             const V3 o = tr.o;
                             const V3 hp = v3(o.x + t * dir.x, o.y + t * dir.y, o.z + t * dir.z);  // :469
-                            const Frame fr = frame_from_normal(sn);  // main.cpp:414
-                            dir = to_world(fr, cosine_hemisphere(xi_x, xi_y));  // main.cpp:418-419, 424
+                            if (kMode == kModeUnit) {
+                                const Frame fr = frame_from_normal(sn);  // main.cpp:414
+                                dir = to_world(fr, cosine_hemisphere(xi_x, xi_y));  // main.cpp:418-419, 424
+                            } else {  // Lambert on triangles as above; spheres / mirror / glass as smallpt
+                                float wgt;
+                                dir = scatter(a.sc, material_kind(a.sc, mat), slot, dir, hp, sn, xi_x, xi_y, wgt);
+                                thr = thr * wgt; thg = thg * wgt; thb = thb * wgt;
+                            }
                             rs = rng.state;
                             depth++;
                             tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit, L);
@@ -964,7 +1034,7 @@ void render_fused_kernel(FusedArgs a) {
                 }
                 if (term) {
                     if (kMode == kModeUnit) {
-                        a.sflag[(size_t)(sample - a.sample0) * a.P + pix] = slot < 0 ? 1 : 0;
+                        a.sflag[(size_t)(sample - a.sample0) * a.P + pix] = slot == -1 ? 1 : 0;
                     } else {
                         float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
                         f[0] = lr;
@@ -1083,9 +1153,30 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
     if (i >= a.n) return;
     const bool m = !a.mask || ((a.mask_size == 1) ? (a.mask[0] != 0) : (a.mask[i] != 0));
     const int32_t id = a.tri_id[i];
-    if (!m || id < 0) return;                                    // active = neq(tri_id,-1) && mask
-    const int32_t slot = a.sc.orig2slot[id];
+    if (!m || id == -1) return;                                  // active = neq(tri_id,-1) && mask
     const float t = a.t[i], u = a.u[i], v = a.v[i];
+    if (id < -1) {  // an analytic sphere (spt_scene_set_spheres): -2 - k
+        const uint32_t k = (uint32_t)(-2 - id);
+        if (k >= a.sc.nsph) return;
+        const float4 sp = a.sc.spheres[k];
+        const V3 p = v3(a.ox[i] + t * a.dx[i], a.oy[i] + t * a.dy[i], a.oz[i] + t * a.dz[i]);
+        const V3 n = normalize(v3(p.x - sp.x, p.y - sp.y, p.z - sp.z));
+        if (a.px) a.px[i] = p.x;
+        if (a.py) a.py[i] = p.y;
+        if (a.pz) a.pz[i] = p.z;
+        if (a.gnx) a.gnx[i] = n.x;
+        if (a.gny) a.gny[i] = n.y;
+        if (a.gnz) a.gnz[i] = n.z;
+        if (a.snx) a.snx[i] = n.x;
+        if (a.sny) a.sny[i] = n.y;
+        if (a.snz) a.snz[i] = n.z;
+        if (a.tcu) a.tcu[i] = 0.0f;
+        if (a.tcv) a.tcv[i] = 0.0f;
+        if (a.mat_id) a.mat_id[i] = a.sc.sph_mat ? a.sc.sph_mat[k] : 0;
+        return;
+    }
+    if (id < 0 || (uint64_t)id >= a.ntri) return;
+    const int32_t slot = a.sc.orig2slot[id];
     // every output plane may be NULL on its own (spt.h spt_hit_info)
     if (a.px) a.px[i] = a.ox[i] + t * a.dx[i];
     if (a.py) a.py[i] = a.oy[i] + t * a.dy[i];
@@ -1200,9 +1291,12 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
 hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
     const dim3 g(blocks_for(grid_items, kShadeBlock)), b(kShadeBlock);
-    if (mode == kModeEmit) hipLaunchKernelGGL(shade_kernel<kModeEmit>, g, b, 0, s, a);
-    else if (mode == kModeAlbedo) hipLaunchKernelGGL(shade_kernel<kModeAlbedo>, g, b, 0, s, a);
-    else hipLaunchKernelGGL(shade_kernel<kModeUnit>, g, b, 0, s, a);
+    const bool spt = a.sc.nsph || a.sc.nkind;  // never in unit mode (spt_render)
+    if (mode == kModeEmit && spt) hipLaunchKernelGGL((shade_kernel<kModeEmit, true>), g, b, 0, s, a);
+    else if (mode == kModeEmit) hipLaunchKernelGGL((shade_kernel<kModeEmit, false>), g, b, 0, s, a);
+    else if (mode == kModeAlbedo && spt) hipLaunchKernelGGL((shade_kernel<kModeAlbedo, true>), g, b, 0, s, a);
+    else if (mode == kModeAlbedo) hipLaunchKernelGGL((shade_kernel<kModeAlbedo, false>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((shade_kernel<kModeUnit, false>), g, b, 0, s, a);
     return hipGetLastError();
 }
 

@@ -62,7 +62,82 @@ struct DeviceScene {
     const uint4* tex_info; // per material: first texel, width, height, 1 if it has an image (null: none)
     uint32_t ntex;         // entries of tex_info
     const float4* texels;  // RGB(-) texels of every image
+    const float4* spheres; // analytic spheres (cx, cy, cz, r), tested after the BVH (null: none)
+    const int32_t* sph_mat;
+    uint32_t nsph;
+    const uint32_t* mat_kind;  // per material SPT_MAT_* (null: every material diffuse)
+    uint32_t nkind;
 };
+
+constexpr uint32_t kMatDiffuse = 0, kMatMirror = 1, kMatGlass = 2;  // SPT_MAT_*
+SPT_HD uint32_t material_kind(const DeviceScene& sc, uint32_t mat) {
+    return (sc.mat_kind && mat < sc.nkind) ? sc.mat_kind[mat] : kMatDiffuse;
+}
+
+// smallpt Sphere::intersect in the ray's own t units (d need not be unit):
+// the nearer root in [tmin, tmax], else +inf.  f32 with the sphere-relative
+// origin; the oracle restates the same operation order.
+SPT_HD float sphere_t(V3 o, V3 d, float4 s, float tmin, float tmax) {
+    const V3 op = v3(s.x - o.x, s.y - o.y, s.z - o.z);
+    const float a = dot(d, d);
+    const float b = dot(op, d);
+    const float c = dot(op, op) - s.w * s.w;
+    const float det = b * b - a * c;
+    if (!(det >= 0.0f)) return INFINITY;
+    const float sq = sqrtf(det);
+    const float t0 = (b - sq) / a, t1 = (b + sq) / a;
+    if (t0 >= tmin && t0 <= tmax) return t0;
+    if (t1 >= tmin && t1 <= tmax) return t1;
+    return INFINITY;
+}
+
+// The new direction of a bounce and its weight.  Triangles with a diffuse
+// material: the reference's Lambert bounce (main.cpp:413-424; Frame3 of the
+// un-normalised shading normal, coordframe.h:17-30, cosine hemisphere,
+// mapping.h:5-11).  Spheres and the mirror / glass kinds follow smallpt's
+// radiance(): the unit normal (a sphere's (x - c) / r direction, a triangle's
+// normalised shading normal) flipped toward the ray for diffuse (nl); SPEC
+// reflects; REFR refracts with index 1.5 and Schlick's Fresnel term, choosing
+// reflection with probability P = 1/4 + Re/2 by xi_x (weight Re/P, else
+// (1 - Re)/(1 - P)); total internal reflection reflects with weight 1.
+SPT_HD V3 scatter(const DeviceScene& sc, uint32_t kind, int32_t slot, V3 d, V3 p, V3 sn, float xi_x, float xi_y,
+                  float& weight) {
+    weight = 1.0f;
+    V3 n;
+    if (slot >= 0) {
+        if (kind == kMatDiffuse) return to_world(frame_from_normal(sn), cosine_hemisphere(xi_x, xi_y));
+        n = normalize(sn);
+    } else {
+        const float4 s = sc.spheres[-2 - slot];
+        n = normalize(v3(p.x - s.x, p.y - s.y, p.z - s.z));
+        if (kind == kMatDiffuse) {
+            const V3 nl = dot(n, d) < 0.0f ? n : v3(-n.x, -n.y, -n.z);
+            return to_world(frame_from_normal(nl), cosine_hemisphere(xi_x, xi_y));
+        }
+    }
+    const V3 dn = normalize(d);
+    const float ndd = dot(n, dn);
+    const float k2 = 2.0f * ndd;
+    const V3 refl = v3(dn.x - n.x * k2, dn.y - n.y * k2, dn.z - n.z * k2);  // r.d - n * 2 * n.dot(r.d)
+    if (kind != kMatGlass) return refl;
+    const bool into = ndd < 0.0f;                       // n.dot(nl) > 0
+    const V3 nl = into ? n : v3(-n.x, -n.y, -n.z);
+    const float nc = 1.0f, nt = 1.5f;
+    const float nnt = into ? nc / nt : nt / nc;
+    const float ddn = dot(dn, nl);
+    const float cos2t = 1.0f - (nnt * nnt) * (1.0f - ddn * ddn);
+    if (cos2t < 0.0f) return refl;                      // total internal reflection
+    const float ks = (into ? 1.0f : -1.0f) * (ddn * nnt + sqrtf(cos2t));
+    const V3 tdir = normalize(v3(dn.x * nnt - n.x * ks, dn.y * nnt - n.y * ks, dn.z * nnt - n.z * ks));
+    const float ea = nt - nc, eb = nt + nc;
+    const float R0 = (ea * ea) / (eb * eb);
+    const float c = 1.0f - (into ? -ddn : dot(tdir, n));
+    const float Re = R0 + (1.0f - R0) * ((((c * c) * c) * c) * c);
+    const float Tr = 1.0f - Re, P = 0.25f + 0.5f * Re;
+    if (xi_x < P) { weight = Re / P; return refl; }
+    weight = Tr / (1.0f - P);
+    return tdir;
+}
 
 // ImageTexture::texel_fetch_wrap / texel_fetch (main.cpp:47-60): clamp, then
 // the reference's index y * size.y + x (main.cpp:52), kept inside the image.
@@ -97,7 +172,7 @@ SPT_HD V3 reflectance(const DeviceScene& sc, uint32_t mat, uint32_t slot, float 
     if (mat < sc.ntex && sc.tex_info[mat].w) {
         const uint4 ti = sc.tex_info[mat];
         float tu = 0.0f, tv = 0.0f;
-        if (sc.tc) {  // barycentric_interpolate (add_math.h:4-7, optix_backend.h:395-401)
+        if (sc.tc && (int32_t)slot >= 0) {  // barycentric_interpolate (add_math.h:4-7, optix_backend.h:395-401); spheres: (0, 0)
             const float* c = sc.tc + (size_t)slot * 6;
             const float w = (1.0f - u) - v;
             tu = (w * c[0] + u * c[2]) + v * c[4];
@@ -214,6 +289,7 @@ struct HitInfoArgs {
     uint32_t mask_size, n;
     float *px, *py, *pz, *gnx, *gny, *gnz, *snx, *sny, *snz, *tcu, *tcv;
     int32_t* mat_id;
+    uint64_t ntri;  // triangle ids >= ntri are skipped
 };
 
 // Tile-local row -> global row for interleaved row groups.

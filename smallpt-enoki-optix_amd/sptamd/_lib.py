@@ -32,8 +32,9 @@ EXPORTED = [
     "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write", "spt_pbrt_load",
     "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
-    "spt_bvh_build_stats", "spt_scene_set_texture",
+    "spt_bvh_build_stats", "spt_scene_set_texture", "spt_scene_set_spheres", "spt_scene_set_material_kinds",
 ]
+SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
 
 
@@ -163,6 +164,8 @@ def _load() -> ctypes.CDLL:
         "spt_scene_get_config": (i32, [vp, POINTER(Config)]),
         "spt_bvh_build_stats": (i32, [vp, u64, POINTER(Config), POINTER(SceneStats)]),
         "spt_scene_set_texture": (i32, [vp, u32, vp, u32, u32]),
+        "spt_scene_set_spheres": (i32, [vp, vp, vp, u32]),
+        "spt_scene_set_material_kinds": (i32, [vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -144,6 +144,22 @@ class HipBackend:
         e = np.ascontiguousarray(np.asarray(emission_rgb, dtype=np.float32).reshape(-1, 3))
         check(lib.spt_scene_set_emission(self._scene, e.ctypes.data, e.shape[0]), "spt_scene_set_emission")
 
+    def set_spheres(self, center_radius=None, material_ids=None) -> None:
+        """smallpt's analytic spheres: (n, 4) (cx, cy, cz, r) float32 and n material ids; None removes them."""
+        if center_radius is None or len(center_radius) == 0:
+            check(lib.spt_scene_set_spheres(self._scene, None, None, 0), "spt_scene_set_spheres")
+            return
+        cr = np.ascontiguousarray(np.asarray(center_radius, dtype=np.float32).reshape(-1, 4))
+        mat = None if material_ids is None else np.ascontiguousarray(np.asarray(material_ids, dtype=np.int32))
+        check(lib.spt_scene_set_spheres(self._scene, cr.ctypes.data, _host_ptr(mat), cr.shape[0]),
+              "spt_scene_set_spheres")
+        self._spheres = (cr, mat)
+
+    def set_material_kinds(self, kinds) -> None:
+        """Per material _lib.SPT_MAT_DIFFUSE / _MIRROR / _GLASS."""
+        k = np.ascontiguousarray(np.asarray(kinds, dtype=np.uint32).reshape(-1))
+        check(lib.spt_scene_set_material_kinds(self._scene, k.ctypes.data, k.size), "spt_scene_set_material_kinds")
+
     def set_texture(self, material: int, image=None) -> None:
         """Material `material`'s reflectance image (ImageTexture, main.cpp:34-80):
         (H, W, 3) float32, or None to remove it."""
@@ -298,6 +314,10 @@ class Scene:
             self.backend.set_albedo(m["albedo"])
         if m.get("emission") is not None:
             self.backend.set_emission(m["emission"])
+        if m.get("spheres") is not None:
+            self.backend.set_spheres(m["spheres"], m.get("sphere_mat"))
+        if m.get("kinds") is not None:
+            self.backend.set_material_kinds(m["kinds"])
 
     def intersect(self, ray: Ray3, active=None):           # main.cpp:320-340
         return self.backend.intersect(ray, active)

@@ -9,6 +9,8 @@
 * ``cornell_spheres`` — smallpt's Cornell box (walls as quads, the two
   spheres and the ceiling light tessellated) for the ray-compaction stress
   configuration.
+* ``smallpt_analytic`` — the same box with smallpt's own analytic spheres:
+  a mirror ball, a glass ball and the big light sphere (SPT_MAT_* kinds).
 * ``city_synth`` — a ~10M-triangle procedural "San-Miguel-class" scene for
   the large-scene configuration.
 
@@ -218,6 +220,45 @@ def cornell_spheres(detail: float = 1.0) -> Dict[str, np.ndarray]:
     p, n, t = _bottom_cap((0.5, 6.816 - 0.0027, 0.816), 6.0, math.radians(2.5), s(64), s(8))
     b.add(p, n, t, t, m_light)
     return b.mesh()
+
+
+def smallpt_analytic(detail: float = 1.0) -> Dict[str, np.ndarray]:
+    """smallpt's scene as smallpt has it (scaled by 1/100): the Cornell walls as
+    triangle quads (cornell_spheres' walls), and the mirror ball, the glass
+    ball and the 600-radius light as analytic spheres (spt_scene_set_spheres)
+    with SPT_MAT_MIRROR / SPT_MAT_GLASS / diffuse-emitting materials
+    (spt_scene_set_material_kinds).  Render with smallpt_materials(), env = 0,
+    cornell_camera().  Extra keys: spheres (3, 4), sphere_mat (3,), kinds."""
+    b = _Builder()
+    m_left = b.material("left", (0.75, 0.25, 0.25))
+    m_right = b.material("right", (0.25, 0.25, 0.75))
+    m_white = b.material("white", (0.75, 0.75, 0.75))
+    m_mirror = b.material("mirror", (0.999, 0.999, 0.999))
+    m_glass = b.material("glass", (0.999, 0.999, 0.999))
+    m_light = b.material("light", (0.0, 0.0, 0.0), (12.0, 12.0, 12.0))
+    s = lambda n: max(1, int(round(n * detail)))  # noqa: E731
+    x0, x1, y0, y1, z0, z1 = 0.01, 0.99, 0.0, 0.816, 0.0, 2.9
+    walls = [
+        ((x0, y0, z0), (0, 0, z1 - z0), (0, y1 - y0, 0), (1, 0, 0), m_left),
+        ((x1, y0, z0), (0, y1 - y0, 0), (0, 0, z1 - z0), (-1, 0, 0), m_right),
+        ((x0, y0, z0), (0, y1 - y0, 0), (x1 - x0, 0, 0), (0, 0, 1), m_white),
+        ((x0, y0, z0), (x1 - x0, 0, 0), (0, 0, z1 - z0), (0, 1, 0), m_white),
+        ((x0, y1, z0), (0, 0, z1 - z0), (x1 - x0, 0, 0), (0, -1, 0), m_white),
+    ]
+    for corner, eu, ev, nrm, m in walls:
+        p, n, t = _quad_grid(corner, eu, ev, s(8), s(8), nrm)
+        b.add(p, n, t, np.zeros_like(t), m)
+    mesh = b.mesh()
+    # smallpt: Sphere(16.5, (27, 16.5, 47), SPEC), Sphere(16.5, (73, 16.5, 78), REFR),
+    # Sphere(600, (50, 681.6 - .27, 81.6), e = 12) — in the same 1/100 units
+    mesh["spheres"] = np.array([[0.27, 0.165, 0.47, 0.165], [0.73, 0.165, 0.78, 0.165],
+                                [0.5, 6.816 - 0.0027, 0.816, 6.0]], np.float32)
+    mesh["sphere_mat"] = np.array([m_mirror, m_glass, m_light], np.int32)
+    kinds = np.zeros(mesh["kd"].shape[0], np.uint32)
+    kinds[m_mirror] = _lib.SPT_MAT_MIRROR
+    kinds[m_glass] = _lib.SPT_MAT_GLASS
+    mesh["kinds"] = kinds
+    return mesh
 
 
 def smallpt_materials(mesh: Dict[str, np.ndarray]):

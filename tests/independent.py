@@ -77,10 +77,39 @@ def _intersect(tris, ox, oy, oz, dx, dy, dz, tmin=1e-3):
     return tri, best, bu, bv
 
 
+def _spheres(sph, ox, oy, oz, dx, dy, dz, tri, best, tmin=1e-3):
+    """smallpt's analytic spheres after the triangles (float64, the textbook
+    quadratic in the ray's own t units): ids -2 - k."""
+    for k in range(sph.shape[0]):
+        cx, cy, cz, r = sph[k]
+        px, py, pz = cx - ox, cy - oy, cz - oz
+        a = dx * dx + dy * dy + dz * dz
+        b = px * dx + py * dy + pz * dz
+        c = px * px + py * py + pz * pz - r * r
+        disc = b * b - a * c
+        with np.errstate(invalid="ignore"):
+            sq = np.sqrt(np.maximum(disc, 0.0))
+        t0, t1 = (b - sq) / a, (b + sq) / a
+        t = np.where(t0 >= tmin, t0, np.where(t1 >= tmin, t1, np.inf))
+        ok = (disc >= 0) & (t < best)
+        best = np.where(ok, t, best)
+        tri = np.where(ok, -2 - k, tri)
+    return tri, best
+
+
+def _reflect(dx, dy, dz, nx, ny, nz):
+    k = 2.0 * (dx * nx + dy * ny + dz * nz)
+    return dx - k * nx, dy - k * ny, dz - k * nz
+
+
 def render(mesh: dict, W: int, H: int, spp: int, depth: int, camera: dict, env=(1.0, 1.0, 1.0), albedo=None,
            emission=None, rr_start_depth: int = 1 << 30, seed: int = 0, samples: bool = False):
     """Mean radiance per pixel, (3, H, W) float64; with samples=True also the
-    per-sample radiance (3, H, W, spp) for variance estimates."""
+    per-sample radiance (3, H, W, spp) for variance estimates.  mesh may carry
+    smallpt's "spheres" / "sphere_mat" and per-material "kinds" (0 diffuse,
+    1 mirror, 2 glass: smallpt's radiance(), with the Fresnel choice made with
+    probability Re and weight 1 — a different unbiased choice from the
+    product's P = 1/4 + Re/2 with weights Re/P, Tr/(1-P))."""
     pos = np.asarray(mesh["pos"], np.float64).reshape(-1, 3)
     pt = np.asarray(mesh["pos_tri"], np.int64).reshape(-1, 3)
     tris = pos[pt]                                                    # (T, 3, 3)
@@ -96,8 +125,10 @@ def render(mesh: dict, W: int, H: int, spp: int, depth: int, camera: dict, env=(
     mat = np.zeros(T, np.int64) if mesh.get("mat_id") is None else np.asarray(mesh["mat_id"], np.int64)
     alb = np.ones((1, 3)) if albedo is None else np.asarray(albedo, np.float64).reshape(-1, 3)
     emi = None if emission is None else np.asarray(emission, np.float64).reshape(-1, 3)
-    mat_a = np.where((mat >= 0) & (mat < alb.shape[0]), mat, 0)
     env = np.asarray(env, np.float64)
+    sph = None if mesh.get("spheres") is None else np.asarray(mesh["spheres"], np.float64).reshape(-1, 4)
+    sph_mat = None if sph is None else np.asarray(mesh["sphere_mat"], np.int64).reshape(-1)
+    kinds = None if mesh.get("kinds") is None else np.asarray(mesh["kinds"], np.int64).reshape(-1)
 
     frm, cx, cy, cz, dist, ratio = _camera(camera, W, H)
     rng = np.random.Generator(np.random.Philox(seed))
@@ -122,11 +153,16 @@ def render(mesh: dict, W: int, H: int, spp: int, depth: int, camera: dict, env=(
     idx = np.arange(N)                                                # live paths
     for j in range(depth):
         tri, t, u, v = _intersect(tris, ox, oy, oz, dx, dy, dz)
-        miss = tri < 0
+        if sph is not None:
+            tri, t = _spheres(sph, ox, oy, oz, dx, dy, dz, tri, t)
+        miss = tri == -1
         L[idx[miss]] += thr[miss] * env                               # main.cpp:407
         hit = ~miss
+        # material per hit (triangles: mat_id; spheres: sphere_mat)
+        mhit = np.where(tri >= 0, mat[np.maximum(tri, 0)],
+                        sph_mat[np.maximum(-2 - tri, 0)] if sph is not None else 0)
         if emi is not None:
-            m = mat[tri[hit]]
+            m = mhit[hit]
             ok = (m >= 0) & (m < emi.shape[0])
             e = np.zeros((int(hit.sum()), 3))
             e[ok] = emi[m[ok]]
@@ -136,9 +172,23 @@ def render(mesh: dict, W: int, H: int, spp: int, depth: int, camera: dict, env=(
         keep = hit
         tri, t, u, v = tri[keep], t[keep], u[keep], v[keep]
         ox, oy, oz, dx, dy, dz = ox[keep], oy[keep], oz[keep], dx[keep], dy[keep], dz[keep]
-        thr, idx = thr[keep], idx[keep]
+        thr, idx, mh = thr[keep], idx[keep], mhit[keep]
+        is_s = tri < -1
+        tt = np.maximum(tri, 0)
         w = 1.0 - u - v
-        n = w[:, None] * vn[tri, 0] + u[:, None] * vn[tri, 1] + v[:, None] * vn[tri, 2]  # un-normalised
+        n = w[:, None] * vn[tt, 0] + u[:, None] * vn[tt, 1] + v[:, None] * vn[tt, 2]  # un-normalised
+        kind = np.zeros(idx.size, np.int64) if kinds is None else np.where(
+            (mh >= 0) & (mh < kinds.size), kinds[np.clip(mh, 0, max(kinds.size - 1, 0))], 0)
+        if sph is not None and is_s.any():
+            hp = np.stack([ox + t * dx, oy + t * dy, oz + t * dz], 1)
+            c = sph[-2 - tri[is_s]]
+            sn = (hp[is_s] - c[:, :3]) / c[:, 3:4]
+            n[is_s] = sn
+        special = is_s | (kind != 0)
+        if special.any():      # smallpt: unit normal, flipped toward the ray for diffuse
+            n[special] = n[special] / np.linalg.norm(n[special], axis=1, keepdims=True)
+            flip = special & (kind == 0) & ((n * np.stack([dx, dy, dz], 1)).sum(1) >= 0)
+            n[flip] = -n[flip]
         nx, ny, nz = n[:, 0], n[:, 1], n[:, 2]
         sign = np.where(ny >= 0, 1.0, -1.0)                           # coordframe.h:17-30
         a = -1.0 / (sign + ny)
@@ -150,11 +200,38 @@ def render(mesh: dict, W: int, H: int, spp: int, depth: int, camera: dict, env=(
         phi = 2.0 * math.pi * r[1]
         ux, uy, uz = np.cos(phi) * sp, np.sqrt(r[0]), np.sin(phi) * sp
         hx, hy, hz = ox + t * dx, oy + t * dy, oz + t * dz
-        dx = bxx * ux + nx * uy + bzx * uz
-        dy = bxy * ux + ny * uy + bzy * uz
-        dz = bxz * ux + nz * uy + bzz * uz
+        ndx = bxx * ux + nx * uy + bzx * uz
+        ndy = bxy * ux + ny * uy + bzy * uz
+        ndz = bxz * ux + nz * uy + bzz * uz
+        if (kind != 0).any():
+            ln = np.sqrt(dx * dx + dy * dy + dz * dz)
+            ux_, uy_, uz_ = dx / ln, dy / ln, dz / ln
+            rx, ry, rz = _reflect(ux_, uy_, uz_, nx, ny, nz)
+            mir = kind == 1
+            ndx, ndy, ndz = np.where(mir, rx, ndx), np.where(mir, ry, ndy), np.where(mir, rz, ndz)
+            gl = kind == 2
+            if gl.any():
+                cosi = ux_ * nx + uy_ * ny + uz_ * nz
+                into = cosi < 0
+                eta = np.where(into, 1.0 / 1.5, 1.5)
+                cn = np.abs(cosi)
+                k = 1.0 - eta * eta * (1.0 - cn * cn)
+                sk = np.sqrt(np.maximum(k, 0.0))
+                nlx, nly, nlz = (np.where(into, nx, -nx), np.where(into, ny, -ny), np.where(into, nz, -nz))
+                tx_ = eta * ux_ + (eta * cn - sk) * nlx
+                ty_ = eta * uy_ + (eta * cn - sk) * nly
+                tz_ = eta * uz_ + (eta * cn - sk) * nlz
+                r0 = (0.5 / 2.5) ** 2
+                cc = 1.0 - np.where(into, cn, sk)                       # cos of the air-side angle
+                re = r0 + (1.0 - r0) * cc ** 5
+                pick = rng.random(idx.size)
+                refl = (k < 0) | (pick < re)
+                ndx = np.where(gl, np.where(refl, rx, tx_), ndx)
+                ndy = np.where(gl, np.where(refl, ry, ty_), ndy)
+                ndz = np.where(gl, np.where(refl, rz, tz_), ndz)
+        dx, dy, dz = ndx, ndy, ndz
         ox, oy, oz = hx, hy, hz
-        thr = thr * alb[mat_a[tri]]                                   # main.cpp:422
+        thr = thr * alb[np.where((mh >= 0) & (mh < alb.shape[0]), mh, 0)]   # main.cpp:422
         if j + 1 >= rr_start_depth:
             q = thr.max(axis=1)
             roll = rng.random(idx.size)

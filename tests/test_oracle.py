@@ -338,3 +338,58 @@ def test_tex1x1_variant_within_tolerance():
     one_alt, _ = O.OracleScene(m, lib=O.variant("tex1x1")).render(p1)
     assert not np.array_equal(one_alt, one)
     np.testing.assert_allclose(one_alt, one, rtol=1e-6, atol=0)
+
+
+def _tiny_far_mesh():
+    """One small triangle far from everything (the spheres do the work)."""
+    return {"pos": np.array([[100, 100, 100], [101, 100, 100], [100, 101, 100]], np.float32),
+            "pos_tri": np.array([[0, 1, 2]], np.int32), "mat_id": np.zeros(1, np.int32)}
+
+
+def test_sphere_intersection_known_answers():
+    """smallpt Sphere::intersect in the ray's t units: from outside the nearer
+    root, from inside the far one, tmin / tmax windows, misses; ids -2 - k."""
+    m = _tiny_far_mesh()
+    sph = np.array([[0, 0, 0, 1], [0, 0, 10, 2]], np.float32)
+    sc = O.OracleScene(m, spheres=sph, sphere_mat=[3, 4])
+    o = np.array([[0, 0, 0, 0, 0, 5], [0, 0, 0, 0, 0, 0], [-5, 0, -5, -5, 10, 0]], np.float32)
+    d = np.array([[0, 1, 0, 0, 0, 0], [0, 0, 0, 0, 0, 1], [2, 0, 2, 2, -1, 0]], np.float32)
+    tmax = np.array([1e20, 1e20, 1.5, 1e20, 1e20, 1e20], np.float32)
+    tmin = np.array([1e-3, 1e-3, 1e-3, 2.5, 1e-3, 1e-3], np.float32)
+    tri, t, _, _ = sc.intersect(o, d, tmin=tmin, tmax=tmax)
+    # 0: outside -> t = (5 - 1) / 2; 1: inside -> t = 1; 2: tmax 1.5 < 2 -> miss;
+    # 3: tmin 2.5 -> far root (5 + 1) / 2; 4: inside sphere 1 (r 2) toward -z -> 2;
+    # 5: from (5, 0, 0) along +y misses both
+    np.testing.assert_array_equal(tri, [-2, -2, -1, -2, -3, -1])
+    np.testing.assert_array_equal(t[[0, 1, 3, 4]], np.float32([2.0, 1.0, 3.0, 2.0]))
+    # any-hit: the same hit / miss answer
+    tri_a, *_ = sc.intersect(o, d, tmin=tmin, tmax=tmax, closest=False)
+    np.testing.assert_array_equal(tri_a != -1, tri != -1)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_emissive_sphere_geometric_series(kind):
+    """The camera inside a sphere that emits Le = 1 with albedo 1/2: a diffuse
+    (nl flipped inward) or mirror wall is hit on every cast, so each sample
+    gathers 1 + 1/2 + ... + 2^(1-D), exact in fp32."""
+    m = _tiny_far_mesh()
+    cam = (0.0, 3.03, 5.0)
+    sph = np.array([[cam[0], cam[1], cam[2], 3.0]], np.float32)
+    sc = O.OracleScene(m, albedo=[[1, 1, 1], [0.5, 0.5, 0.5]], emission=[[0, 0, 0], [1, 1, 1]],
+                       spheres=sph, sphere_mat=[1], kinds=np.array([0, kind], np.uint32))
+    for depth in (1, 5):
+        f, casts = sc.render(O.reference_params(10, 8, 3, depth, rr_start_depth=depth, env=(0, 0, 0)))
+        assert casts == 10 * 8 * 3 * depth
+        assert np.all(f == np.float32(2.0 - 2.0 ** (1 - depth))), (kind, depth)
+
+
+def test_glass_sphere_conserves_energy():
+    """The camera inside a clear glass ball under a unit sky: Fresnel splits
+    only redistribute weight (Re/P, Tr/(1-P)), so the image's expectation is
+    the probability of escaping within the cast budget, ~1 at depth 24."""
+    m = _tiny_far_mesh()
+    sph = np.array([[0.0, 3.03, 5.0, 0.5]], np.float32)
+    sc = O.OracleScene(m, spheres=sph, sphere_mat=[1], kinds=np.array([0, 2], np.uint32))
+    f, _ = sc.render(O.reference_params(16, 16, 64, 24, rr_start_depth=99, env=(1, 1, 1)))
+    assert abs(f.mean() - 1.0) < 0.03, f.mean()
+    assert f.std() > 0.05      # the weights differ per sample

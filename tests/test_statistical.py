@@ -71,3 +71,29 @@ def test_oracle_matches_independent_estimator_emitters():
     z, zimg = block_z(got.astype(np.float64), mean_b, per_b)
     assert z.max() <= Z_MAX, z.max()
     assert zimg.max() <= Z_MAX, zimg
+
+
+def test_oracle_matches_independent_estimator_smallpt_spheres():
+    """smallpt's own scene: analytic mirror and glass balls and the light
+    sphere (smallpt.cpp radiance(): SPEC, REFR with Schlick's Fresnel term).
+    The estimator picks reflection with probability Re at weight 1, the oracle
+    with P = 1/4 + Re/2 at weight Re/P or Tr/(1-P): the same expectation.
+    Swapping the two balls' kinds must fail the same test (sensitivity)."""
+    from sptamd import scenes
+    m = scenes.smallpt_analytic(detail=0.125)
+    alb, emi = scenes.smallpt_materials(m)
+    cam = scenes.cornell_camera()
+    W = H = 32
+    spp, depth = 512, 6
+    kw = dict(env=(0.0, 0.0, 0.0), rr_start_depth=3)
+    mean_b, per_b = I.render(m, W, H, spp, depth, cam, albedo=alb, emission=emi, seed=5, samples=True, **kw)
+    got, _ = O.OracleScene(m, albedo=alb, emission=emi).render(O.reference_params(W, H, spp, depth, camera=cam, **kw))
+    z, zimg = block_z(got.astype(np.float64), mean_b, per_b)
+    assert z.max() <= Z_MAX, z.max()
+    assert zimg.max() <= Z_MAX, zimg
+    swapped = m["kinds"].copy()
+    swapped[m["sphere_mat"][0]], swapped[m["sphere_mat"][1]] = m["kinds"][m["sphere_mat"][1]], m["kinds"][m["sphere_mat"][0]]
+    bad, _ = O.OracleScene(m, albedo=alb, emission=emi, kinds=swapped).render(
+        O.reference_params(W, H, spp, depth, camera=cam, **kw))
+    zb, _ = block_z(bad.astype(np.float64), mean_b, per_b)
+    assert zb.max() > Z_MAX, zb.max()

@@ -46,6 +46,11 @@ for s in "$@"; do
     pmc1s) run pmc1s 900 env SPT_STREAMS=1 CONFIG=1 bash tools/pmc_isect.sh gpurun_out/pmc1s ;;
     prof1s) run prof1s 600 env SPT_STREAMS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1s -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
+    trav4) run trav4 600 python tools/trav_stats.py --city --depths 8 --spp 8 ;;
+    trav4h) run trav4h 600 env SPT_BUILD=host python tools/trav_stats.py --city --depths 8 --spp 8 ;;
+    bench4h) run bench4h 600 env SPT_BUILD=host python bench.py --config 4 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    tilesimw) run tilesimw 400 python tools/tile_sim.py --tiles 1 2 4 8 --pipeline wavefront --timing ;;
+    tilesima) run tilesima 400 python tools/tile_sim.py --tiles 1 2 4 8 --timing ;;
     tilesim) run tilesim 400 python tools/tile_sim.py ;;
     tilesimt) run tilesimt 400 python tools/tile_sim.py --timing ;;
     tilesimf) run tilesimf 400 python tools/tile_sim.py --pipeline fused ;;

@@ -25,13 +25,21 @@ def main():
     ap.add_argument("--depths", type=int, nargs="+", default=[1, 2, 8])
     ap.add_argument("--scene", default="mitsuba_synth")
     ap.add_argument("--wavefront", type=int, default=0)
+    ap.add_argument("--city", action="store_true", help="BASELINE config 4: the 10M-triangle pbrt city, 1920x1080")
     a = ap.parse_args()
     sc = sptamd.Scene()
-    sc.add_triangle_mesh(scenes.scene_obj(a.scene))
+    kw = {}
+    W = H = a.size
+    if a.city:
+        sc.add_triangle_mesh(scenes.scene_pbrt("city_synth"))
+        kw["camera"] = sc.pbrt_info["camera"]
+        W, H = 1920, 1080
+    else:
+        sc.add_triangle_mesh(scenes.scene_obj(a.scene))
     sc.commit(0)
     print(json.dumps({"bvh": sc.backend.stats}))
     for D in a.depths:
-        p = sptamd.make_params(a.size, a.size, a.spp, D, timing=True, wavefront_paths=a.wavefront)
+        p = sptamd.make_params(W, H, a.spp, D, timing=True, wavefront_paths=a.wavefront, **kw)
         sc.render(p)
         _, st = sc.render(p)
         p.flags = _lib.SPT_FLAG_TRAVERSAL_STATS
