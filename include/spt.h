@@ -129,7 +129,7 @@ typedef struct spt_scene_stats {
     uint64_t ntri, nodes, leaves;
     uint32_t max_depth;         /* BVH depth (sets the LDS stack depth) */
     uint32_t max_leaf;
-    uint32_t bvh_width;         /* 8: compressed 8-wide BVH (default), 2: BVH2 (spt_config.bvh_width) */
+    uint32_t bvh_width;         /* 8 / 6: compressed 8-wide / 64-B 6-wide BVH, 2: BVH2 (spt_config.bvh_width) */
     uint32_t builder;           /* SPT_BUILD_HOST_SAH or SPT_BUILD_GPU_PLOC: the build that ran */
     uint64_t device_bytes;
     double build_ms;            /* BVH build (host SAH, or GPU PLOC + collapse, synchronised) */
@@ -193,7 +193,8 @@ enum {
 typedef struct spt_config {
     /* --- scene build (spt_scene_create_cfg) */
     uint32_t build;                 /* spt_build (AUTO: GPU from gpu_build_min_tris up)      [0..2] */
-    uint32_t bvh_width;             /* 8: compressed BVH8 (default), 2: BVH2 (host build)   {2, 8} */
+    uint32_t bvh_width;             /* 8: compressed BVH8 (80-B nodes), 6: at most six
+                                       children in one 64-B node, 2: BVH2 (host build) {2, 6, 8} */
     uint64_t gpu_build_min_tris;    /* SPT_BUILD_AUTO threshold, 2,000,000                          */
     uint32_t collapse;              /* BVH8 collapse: 0 SAH-optimal DP (default), 1 greedy    [0..1] */
     uint32_t ploc_radius;           /* GPU PLOC search radius                        {8, 16, 32, 64} */
@@ -277,7 +278,7 @@ spt_status spt_scene_get_stats(spt_scene scene, spt_scene_stats* out);
 
 /* The host builders alone, without a device (diagnostics; the host sanitizer
  * run drives the builders through it): triangle soup tri_verts (ntri x 9
- * floats: v0 v1 v2), cfg->bvh_width 2 or 8 and cfg->collapse (NULL =
+ * floats: v0 v1 v2), cfg->bvh_width 2, 6 or 8 and cfg->collapse (NULL =
  * defaults).  Fills ntri, nodes, leaves, max_depth, max_leaf, bvh_width,
  * builder (SPT_BUILD_HOST_SAH), build_ms and sah_cost; device_bytes = 0. */
 spt_status spt_bvh_build_stats(const float* tri_verts, uint64_t ntri, const spt_config* cfg,

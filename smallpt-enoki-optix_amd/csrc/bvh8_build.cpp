@@ -4,6 +4,8 @@
 // HPG 2017): the SAH-optimal collapse of their §3.1 by dynamic programming
 // (default; the greedy "open the largest-area inner child until 8 children"
 // is mode 1), octant-ordered child slots, 8-bit conservative quantisation.
+// width 6 caps a node at six children (still in eight octant slots) for the
+// 64-B device node (gpu_bvh8_holes).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -43,6 +45,7 @@ struct Collapser {
     std::vector<double> cost, dist;
     std::vector<uint8_t> take, split;
     double c_node = 1.0, c_prim = 0.3;
+    int width = 8;                         // children per node: 8, or 6 for the 64-B device node
 
     uint32_t count_tris(int32_t code) {
         if (code < 0) return ((~(uint32_t)code) & 7u) + 1u;
@@ -122,7 +125,7 @@ struct Collapser {
             const Kid l = child(n, 0), r = child(n, 1);
             double* C = &cost[(size_t)n * 9];
             double* D = &dist[(size_t)n * 9];
-            for (int i = 2; i <= 8; i++) {
+            for (int i = 2; i <= width; i++) {
                 split[(size_t)n * 9 + i] = 1;  // a valid share even when every cost is inf / NaN
                 for (int k = 1; k < i; k++) {
                     const double v = kid_cost(l, k) + kid_cost(r, i - k);
@@ -133,10 +136,10 @@ struct Collapser {
             self.code = n;
             self.ntri = ntri2[n];
             const double lc = self.ntri <= 3 ? (double)area[n] * c_prim * (double)self.ntri : INFINITY;
-            const double ic = (double)area[n] * c_node + D[8];
+            const double ic = (double)area[n] * c_node + D[width];
             C[1] = std::min(lc, ic);
             take[(size_t)n * 9 + 1] = (self.ntri <= 3 && lc <= ic) ? 1 : 0;
-            for (int i = 2; i <= 8; i++) {
+            for (int i = 2; i <= width; i++) {
                 take[(size_t)n * 9 + i] = C[i - 1] <= D[i] ? 1 : 0;
                 C[i] = std::min(C[i - 1], D[i]);
             }
@@ -164,9 +167,9 @@ struct Collapser {
     }
     std::vector<Kid> dp_kids(int32_t node) const {
         std::vector<Kid> kids;
-        const int s = split[(size_t)node * 9 + 8];
+        const int s = split[(size_t)node * 9 + width];
         collect(child(node, 0), s, kids);
-        collect(child(node, 1), 8 - s, kids);
+        collect(child(node, 1), width - s, kids);
         return kids;
     }
 
@@ -177,7 +180,7 @@ struct Collapser {
         // Greedy collapse: open the largest-area kid that cannot be a leaf while
         // room remains; in mode 2 then keep splitting multi-triangle leaf
         // candidates (largest first) to fill the 8 slots.
-        while (mode < 3 && kids.size() < 8) {
+        while (mode < 3 && kids.size() < (size_t)width) {
             int best = -1;
             double best_area = -1.0;
             for (size_t i = 0; i < kids.size(); i++)
@@ -323,7 +326,7 @@ struct Collapser {
 
 }  // namespace
 
-Bvh8BuildResult build_bvh8(const float* tv, uint64_t ntri, bool greedy) {
+Bvh8BuildResult build_bvh8(const float* tv, uint64_t ntri, bool greedy, int width) {
     Bvh8BuildResult res;
     if (ntri == 0) return res;
     // 3: SAH-optimal collapse (+6 % on config 1 over the greedy mode 1)
@@ -331,6 +334,7 @@ Bvh8BuildResult build_bvh8(const float* tv, uint64_t ntri, bool greedy) {
     BvhBuildResult b2 = build_bvh(tv, ntri, mode >= 1 ? 1 : 3);
     Collapser col{b2.nodes, b2.slot2tri, {}, {}, 0, 0};
     col.mode = mode;
+    col.width = width == 6 ? 6 : 8;
     col.ntri2.assign(b2.nodes.size() / 16, 0);
     {
         int32_t r0, r1;

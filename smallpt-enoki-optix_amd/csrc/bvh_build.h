@@ -48,6 +48,18 @@ struct Bvh8BuildResult {
     double sah_cost = 0.0;           // of the underlying BVH2
 };
 // greedy: the greedy collapse instead of the SAH-optimal dynamic program.
-Bvh8BuildResult build_bvh8(const float* tri_verts, uint64_t ntri, bool greedy = false);
+// width: at most 8 children per node, or 6 (the 64-B device node below).
+Bvh8BuildResult build_bvh8(const float* tri_verts, uint64_t ntri, bool greedy = false, int width = 8);
+
+// 64-B device node (gpu_bvh8_holes with width 6; kernels.hip Tracer8T<..., 6>):
+// at most six children, physical index p in slot order; one 64-B half-line
+// per visit instead of the 80-B node's two.  16 words:
+//   w0-2  p.xyz        quantisation origin (f32)
+//   w3    tri_base
+//   w4    meta[0..3]   (as above: inner 0b001_(24+s) with s its octant slot)
+//   w5    meta[4] | meta[5]<<8 | ex<<16 | ey<<24
+//   w6    group | ez<<24    group = first child slot / 8 (child s at 8 * group + s)
+//   w7-12 qlo.x qhi.x qlo.y qhi.y qlo.z qhi.z of children 0..3 (one byte each)
+//   w13-15 per axis x, y, z: lo4 | lo5<<8 | hi4<<16 | hi5<<24
 
 }  // namespace spt

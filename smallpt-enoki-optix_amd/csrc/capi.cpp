@@ -141,6 +141,7 @@ struct spt_scene_t {
     uint64_t ntri = 0;
     float4* nodes = nullptr;
     uint4* nodes8 = nullptr;
+    uint32_t node6 = 0;  // nodes8 holds the 64-B six-wide nodes (spt_config.bvh_width 6)
     float4* tris = nullptr;
     float4* snrm = nullptr;
     float* tc = nullptr;
@@ -168,7 +169,7 @@ struct spt_scene_t {
 
     DeviceScene dev() const {
         DeviceScene d;
-        d.nodes = nodes; d.nodes8 = nodes8; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
+        d.nodes = nodes; d.nodes8 = nodes8; d.node6 = node6; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
         d.albedo = albedo; d.nmat = nmat; d.emission = emission; d.nemit = nemit; d.stack_depth = stack_depth; d.empty = ntri == 0;
         d.tex_info = tex_info; d.ntex = ntex; d.texels = texels;
         d.spheres = spheres; d.sph_mat = sph_mat; d.nsph = nsph;
@@ -294,7 +295,8 @@ spt_status check_config(const spt_config& c) {
         return fail(SPT_ERR_INVALID, "spt_config.%s = %llu outside [%llu, %llu]", #f, (unsigned long long)c.f, \
                     (unsigned long long)(lo), (unsigned long long)(hi));
     CFG_RANGE(build, 0, SPT_BUILD_GPU_PLOC)
-    if (c.bvh_width != 2 && c.bvh_width != 8) return fail(SPT_ERR_INVALID, "spt_config.bvh_width must be 2 or 8");
+    if (c.bvh_width != 2 && c.bvh_width != 6 && c.bvh_width != 8)
+        return fail(SPT_ERR_INVALID, "spt_config.bvh_width must be 2, 6 or 8");
     CFG_RANGE(collapse, 0, 1)
     if (c.ploc_radius != 8 && c.ploc_radius != 16 && c.ploc_radius != 32 && c.ploc_radius != 64)
         return fail(SPT_ERR_INVALID, "spt_config.ploc_radius must be 8, 16, 32 or 64");
@@ -344,7 +346,8 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     hipStream_t s = nullptr;  // the null stream: scene creation is synchronous
     HIP_TRY(gpu_mesh_soup(m, raw.tv, s));
     GpuBvh8 g;
-    HIP_TRY(gpu_build_bvh8(raw.tv, (uint32_t)ntri, s, &g, (int)cfg.ploc_radius, cfg.collapse == 1));
+    const int width = (int)cfg.bvh_width;
+    HIP_TRY(gpu_build_bvh8(raw.tv, (uint32_t)ntri, s, &g, (int)cfg.ploc_radius, cfg.collapse == 1, width));
     spt_scene_t* sc = new spt_scene_t();
     sc->cfg = cfg;
     (void)hipGetDevice(&sc->device);
@@ -353,7 +356,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     uint32_t nslots = 0;
     {
         uint32_t* holes = nullptr;
-        const hipError_t he = gpu_bvh8_holes(g.nodes8, g.nnodes, s, &holes, &nslots);
+        const hipError_t he = gpu_bvh8_holes(g.nodes8, g.nnodes, s, &holes, &nslots, width);
         (void)hipFree(g.nodes8);
         if (he) {
             (void)hipFree(g.slot2tri);
@@ -362,6 +365,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
                         hipGetErrorString(he));
         }
         sc->nodes8 = (uint4*)holes;
+        sc->node6 = width == 6;
     }
     auto bail = [&](hipError_t e) {
         (void)hipFree(g.slot2tri);
@@ -393,9 +397,9 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     ss.leaves = g.leaves;
     ss.max_depth = g.depth;
     ss.max_leaf = 3;
-    ss.bvh_width = 8;
+    ss.bvh_width = (uint32_t)width;
     ss.builder = SPT_BUILD_GPU_PLOC;
-    ss.device_bytes = (uint64_t)nslots * kNode8Quads * 16 + ntri * 3 * 16 * 2 + (with_tc ? ntri * 24 : 0) + ntri * 4;
+    ss.device_bytes = (uint64_t)nslots * (width == 6 ? kNode6Quads : kNode8Quads) * 16 + ntri * 3 * 16 * 2 + (with_tc ? ntri * 24 : 0) + ntri * 4;
     ss.build_ms = now_ms() - t0;
     ss.sah_cost = g.sah_cost;
     *out = sc;
@@ -495,7 +499,8 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
     if (st) return st;
     uint32_t build = cfg.build;
     if (build == SPT_BUILD_AUTO) build = ntri >= cfg.gpu_build_min_tris ? SPT_BUILD_GPU_PLOC : SPT_BUILD_HOST_SAH;
-    const bool use8 = cfg.bvh_width == 8;
+    const bool use8 = cfg.bvh_width != 2;  // compressed wide BVH (8 or 6 children per node)
+    const int width = (int)cfg.bvh_width;
     if (build == SPT_BUILD_GPU_PLOC && !use8) build = SPT_BUILD_HOST_SAH;  // the GPU builder makes BVH8 only
     const double t0 = now_ms();
     const bool host = build == SPT_BUILD_HOST_SAH;
@@ -531,7 +536,7 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
     BvhBuildResult bvh;
     Bvh8BuildResult bvh8;
     if (use8)
-        bvh8 = build_bvh8(tv.data(), ntri, cfg.collapse == 1);
+        bvh8 = build_bvh8(tv.data(), ntri, cfg.collapse == 1, width);
     else
         bvh = build_bvh(tv.data(), ntri);
     const std::vector<uint32_t>& slot2tri = use8 ? bvh8.slot2tri : bvh.slot2tri;
@@ -587,10 +592,10 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
         if (!us) us = upload(&compact, padded.data(), padded.size() * sizeof(uint32_t));
         if (!us) {
             uint32_t* holes = nullptr;
-            const hipError_t he = gpu_bvh8_holes(compact, (uint32_t)nn, nullptr, &holes, &nslots);
+            const hipError_t he = gpu_bvh8_holes(compact, (uint32_t)nn, nullptr, &holes, &nslots, width);
             if (he) us = fail(he == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP,
                               "spt_scene_create (BVH8 layout): %s", hipGetErrorString(he));
-            else sc->nodes8 = (uint4*)holes;
+            else { sc->nodes8 = (uint4*)holes; sc->node6 = width == 6; }
         }
         hfree(compact);
     } else {
@@ -613,8 +618,8 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
     ss.leaves = use8 ? bvh8.leaves : bvh.leaves;
     ss.max_depth = use8 ? bvh8.depth : bvh.max_depth;
     ss.max_leaf = use8 ? 3 : bvh.max_leaf;
-    ss.bvh_width = use8 ? 8 : 2;
-    ss.device_bytes = (use8 ? (uint64_t)nslots * kNode8Quads * 16 : bvh.nodes.size() * 4) +
+    ss.bvh_width = (uint32_t)width;
+    ss.device_bytes = (use8 ? (uint64_t)nslots * (width == 6 ? kNode6Quads : kNode8Quads) * 16 : bvh.nodes.size() * 4) +
                       (h_tris.size() + h_snrm.size()) * 16 +
                       h_tc.size() * 4 + h_o2s.size() * 4;
     ss.build_ms = t1 - t0;
@@ -660,7 +665,7 @@ void spt_default_config(spt_config* c) {
     if (!c) return;
     std::memset(c, 0, sizeof(*c));
     c->build = SPT_BUILD_AUTO;
-    c->bvh_width = 8;
+    c->bvh_width = 6;
     c->gpu_build_min_tris = 2000000;
     c->collapse = 0;
     c->ploc_radius = 16;
@@ -804,8 +809,8 @@ spt_status spt_bvh_build_stats(const float* tv, uint64_t ntri, const spt_config*
     if (st) return st;
     spt_scene_stats ss{};
     const double t0 = now_ms();
-    if (cfg.bvh_width == 8) {
-        const Bvh8BuildResult b = build_bvh8(tv, ntri, cfg.collapse == 1);
+    if (cfg.bvh_width != 2) {
+        const Bvh8BuildResult b = build_bvh8(tv, ntri, cfg.collapse == 1, (int)cfg.bvh_width);
         ss.nodes = b.nodes.size() / 20; ss.leaves = b.leaves; ss.max_depth = b.depth; ss.max_leaf = 3;
         ss.sah_cost = b.sah_cost;
         if (b.slot2tri.size() != ntri) return fail(SPT_ERR_HIP, "spt_bvh_build_stats: BVH8 lost triangles");

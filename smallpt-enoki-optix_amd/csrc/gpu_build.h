@@ -20,9 +20,9 @@ struct GpuBvh8 {
 // d_tv: device, ntri x 9 floats (v0 v1 v2).  On success the caller owns
 // out->nodes8 and out->slot2tri (hipFree).  Synchronises stream s.
 // radius: PLOC search radius (8, 16, 32 or 64); greedy: greedy collapse
-// instead of the SAH-optimal one.
+// instead of the SAH-optimal one; width: at most 8 or 6 children per node.
 hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out, int radius = 16,
-                          bool greedy = false);
+                          bool greedy = false, int width = 8);
 
 // Re-lays a compact BVH8 (both builders' output: nnodes nodes of kNode8Quads
 // quads, the inner children of a node contiguous from w4 in slot order) so
@@ -31,8 +31,11 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
 // ("holes").  The traversal then finds a child without a popcount and keeps
 // one word per stack entry (hit bits + w4 / 8).  Root stays at slot 0.  On
 // success the caller owns *out (device, *nslots nodes).  Synchronises s.
+// width 6: every node has at most six children and is re-encoded as the
+// 64-B node of bvh_build.h (kNode6Quads quads per slot); else copied as is
+// (kNode8Quads quads per slot).
 hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t nnodes, hipStream_t s, uint32_t** out,
-                          uint32_t* nslots);
+                          uint32_t* nslots, int width = 8);
 
 }  // namespace spt
 

@@ -253,7 +253,7 @@ __device__ __forceinline__ float dp_kid_cost(const DpNode* __restrict__ dp, cons
 __global__ __launch_bounds__(kBlock) void dp_kernel(const float4* __restrict__ lo, const float4* __restrict__ hi,
                                                     const int2* __restrict__ kids2, const uint32_t* __restrict__ ntris,
                                                     uint32_t ntri, uint32_t first, uint32_t count,
-                                                    DpNode* __restrict__ dp) {
+                                                    DpNode* __restrict__ dp, int width) {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= count) return;
     const uint32_t n = first + j;
@@ -261,8 +261,8 @@ __global__ __launch_bounds__(kBlock) void dp_kernel(const float4* __restrict__ l
     const uint32_t l = (uint32_t)c.x, r = (uint32_t)c.y;
     float cl[9], cr[9];
     for (int i = 1; i <= 8; i++) {
-        cl[i] = dp_kid_cost(dp, lo, hi, ntri, l, i);
-        cr[i] = dp_kid_cost(dp, lo, hi, ntri, r, i);
+        cl[i] = i <= width ? dp_kid_cost(dp, lo, hi, ntri, l, i) : INFINITY;
+        cr[i] = i <= width ? dp_kid_cost(dp, lo, hi, ntri, r, i) : INFINITY;
     }
     float D[9];
     uint32_t split = 0;
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void dp_kernel(const float4* __restrict__ l
     }
     const float area = 2.0f * half_area(lo[n], hi[n]);
     const float lc = ntris[n] <= kLeafMaxTris ? area * kCPrim * (float)ntris[n] : INFINITY;
-    const float ic = area * kCNode + D[8];
+    const float ic = area * kCNode + D[width];
     DpNode out;
     out.cost[0] = fminf(lc, ic);
     // a leaf only when it may be one (with overflowing areas both costs are inf)
@@ -302,6 +302,7 @@ struct CollapseArgs {
     uint32_t* kids8;         // [count][8] chosen BVH2 children | kLeafKid, 0xffffffff = empty
     uint64_t* counts;        // inner << 32 | leaf triangles
     const DpNode* dp;        // SAH-optimal decisions (null: greedy collapse)
+    uint32_t width;          // children per node: 8, or 6 (the 64-B device node)
 };
 
 constexpr uint32_t kLeafKid = 0x80000000u;  // kids8 flag: the child becomes a BVH8 leaf
@@ -325,8 +326,8 @@ __global__ __launch_bounds__(kBlock) void collapse_pick_kernel(CollapseArgs a) {
         // collect(element, slots), left child first, with an explicit stack
         uint32_t sn[8], si[8], sp = 0;
         const int2 c = a.kids2[root];
-        const uint32_t s8 = (a.dp[root - a.ntri].split >> 18) & 7u;
-        sn[sp] = (uint32_t)c.y; si[sp++] = 8u - s8;
+        const uint32_t s8 = (a.dp[root - a.ntri].split >> (3u * (a.width - 2u))) & 7u;
+        sn[sp] = (uint32_t)c.y; si[sp++] = a.width - s8;
         sn[sp] = (uint32_t)c.x; si[sp++] = s8;
         while (sp) {
             const uint32_t x = sn[--sp];
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(kBlock) void collapse_pick_kernel(CollapseArgs a) {
         k[nk++] = (uint32_t)c.x;
         k[nk++] = (uint32_t)c.y;
     }
-    while (!a.dp && nk < 8 && root >= a.ntri) {
+    while (!a.dp && nk < a.width && root >= a.ntri) {
         int best = -1;
         float ba = -1.0f;
         for (uint32_t i = 0; i < nk; i++)
@@ -576,13 +577,59 @@ __global__ __launch_bounds__(kBlock) void holes_copy_kernel(const uint32_t* __re
     dst[1] = w1;
 }
 
+// width 6: the same re-lay, each node re-encoded as the 64-B node of
+// bvh_build.h — its (at most six) non-empty slots become children 0..5 in
+// slot order, with their meta bytes and planes; unused children get meta 0.
+// A node with more than six children sets *bad (the build used width 8).
+__global__ __launch_bounds__(kBlock) void holes_copy6_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
+                                                             const uint32_t* __restrict__ group,
+                                                             const uint32_t* __restrict__ newidx,
+                                                             uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* w = nodes + (size_t)i * kNode8Quads * 4;
+    uint32_t meta[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t q[6][6];  // [plane lo.x hi.x lo.y hi.y lo.z hi.z][child]
+    for (int p = 0; p < 6; p++)
+        for (int c = 0; c < 6; c++) q[p][c] = (p & 1) ? 0u : 255u;  // empty: inverted
+    uint32_t c = 0;
+    for (uint32_t s = 0; s < 8; s++) {
+        const uint32_t m = (w[6 + (s >> 2)] >> ((s & 3u) * 8u)) & 0xffu;
+        if (!m) continue;
+        if (c == 6) { *bad = 1u; return; }
+        meta[c] = m;
+        for (uint32_t ax = 0; ax < 3; ax++) {
+            q[2 * ax][c] = (w[8 + 2 * ax + (s >> 2)] >> ((s & 3u) * 8u)) & 0xffu;
+            q[2 * ax + 1][c] = (w[14 + 2 * ax + (s >> 2)] >> ((s & 3u) * 8u)) & 0xffu;
+        }
+        c++;
+    }
+    const uint32_t ew = w[3];
+    const uint32_t grp = (ew >> 24) ? group[i] + 1u : 0u;  // first child slot / 8
+    uint32_t o[16];
+    o[0] = w[0]; o[1] = w[1]; o[2] = w[2];
+    o[3] = w[5];
+    o[4] = meta[0] | meta[1] << 8 | meta[2] << 16 | meta[3] << 24;
+    o[5] = meta[4] | meta[5] << 8 | (ew & 0xffu) << 16 | ((ew >> 8) & 0xffu) << 24;
+    o[6] = grp | ((ew >> 16) & 0xffu) << 24;
+    for (uint32_t p = 0; p < 6; p++) o[7 + p] = q[p][0] | q[p][1] << 8 | q[p][2] << 16 | q[p][3] << 24;
+    for (uint32_t ax = 0; ax < 3; ax++)
+        o[13 + ax] = q[2 * ax][4] | q[2 * ax][5] << 8 | q[2 * ax + 1][4] << 16 | q[2 * ax + 1][5] << 24;
+    uint4* dst = (uint4*)(out + (size_t)newidx[i] * kNode6Quads * 4);
+    for (uint32_t k = 0; k < 4; k++) dst[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+}
+
 }  // namespace
 
-hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, uint32_t** out, uint32_t* nslots) {
+hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, uint32_t** out, uint32_t* nslots,
+                          int width) {
     *out = nullptr;
     *nslots = 0;
     Temp tmp;
-    uint32_t *flags, *group, *newidx;
+    uint32_t *flags, *group, *newidx, *bad;
+    const uint32_t quads = width == 6 ? kNode6Quads : kNode8Quads;
+    GB_TRY(tmp.get(&bad, 1));
+    GB_TRY(hipMemsetAsync(bad, 0, sizeof(uint32_t), s));
     GB_TRY(tmp.get(&flags, n));
     GB_TRY(tmp.get(&group, n));
     GB_TRY(tmp.get(&newidx, n));
@@ -604,14 +651,23 @@ hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, ui
     if (groups >= (1u << 24)) return hipErrorInvalidValue;  // w4 / 8 must fit the 24-bit stack field
     const size_t slots = 8 * ((size_t)groups + 1);
     uint32_t* o = nullptr;
-    GB_TRY(dmalloc(&o, slots * kNode8Quads * 4));
-    hipError_t e = hipMemsetAsync(o, 0, slots * kNode8Quads * 16, s);
+    GB_TRY(dmalloc(&o, slots * quads * 4));
+    hipError_t e = hipMemsetAsync(o, 0, slots * quads * 16, s);
     if (!e && n) {
         hipLaunchKernelGGL(holes_index_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx);
-        hipLaunchKernelGGL(holes_copy_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx, o);
+        if (width == 6)
+            hipLaunchKernelGGL(holes_copy6_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx, o,
+                               bad);
+        else
+            hipLaunchKernelGGL(holes_copy_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx, o);
         e = hipGetLastError();
     }
     if (!e) e = hipStreamSynchronize(s);
+    if (!e && width == 6) {
+        uint32_t hb = 0;
+        e = hipMemcpy(&hb, bad, sizeof(hb), hipMemcpyDeviceToHost);
+        if (!e && hb) e = hipErrorInvalidValue;  // a node with more than six children
+    }
     if (e) {
         (void)hipFree(o);
         return e;
@@ -621,7 +677,9 @@ hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, ui
     return hipSuccess;
 }
 
-hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out, int radius, bool greedy) {
+hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBvh8* out, int radius, bool greedy,
+                          int width) {
+    width = width == 6 ? 6 : 8;
     *out = GpuBvh8();
     if (ntri == 0) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
@@ -723,7 +781,7 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
         GB_TRY(tmp.get(&dp, ntri - 1));
         for (const auto& m : made)
             hipLaunchKernelGGL(dp_kernel, dim3(blocks(m.second)), dim3(kBlock), 0, s, lo, hi, kids2, ntris, ntri,
-                               m.first, m.second, dp);
+                               m.first, m.second, dp, width);
         GB_TRY(hipGetLastError());
     }
 
@@ -745,7 +803,7 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
     void* scan8_ws = nullptr;
     hipError_t err = tmp.get((char**)&scan8_ws, scan8_bytes);
     while (err == hipSuccess && count > 0) {
-        CollapseArgs c{lo, hi, kids2, ntris, ntri, queue[q], count, kids8, counts, dp};
+        CollapseArgs c{lo, hi, kids2, ntris, ntri, queue[q], count, kids8, counts, dp, (uint32_t)width};
         hipLaunchKernelGGL(collapse_pick_kernel, dim3(blocks(count)), dim3(kBlock), 0, s, c);
         if ((err = hipGetLastError())) break;
         if ((err = hipcub::DeviceScan::ExclusiveSum(scan8_ws, scan8_bytes, counts, scan, (int)count, s))) break;

@@ -10,6 +10,14 @@
 
 namespace spt {
 
+// minimum waves per SIMD the isect kernels are compiled for (register budget)
+#ifndef SPT_ISECT_WAVES
+#define SPT_ISECT_WAVES 1
+#endif
+#ifndef SPT_ISECT_WAVES6
+#define SPT_ISECT_WAVES6 8
+#endif
+
 // ------------------------------------------------------------- traversal
 // woop_test's double-precision fallback re-reads the triangle (rare path) so
 // the single-precision path need not keep the sheared vertices live.
@@ -101,6 +109,7 @@ __device__ __forceinline__ void slab(float p0, float p1, float o, float inv, flo
 }
 
 struct Tracer {
+    static constexpr int kMinWaves = 1;
     WoopRay wr;
     V3 o;
     float ix, iy, iz, tmin;
@@ -222,8 +231,15 @@ constexpr float kMinDir = 1e-20f;
 // record (slot, id, u, v) live in LDS, one 16-B record each per lane after the
 // stack (ds_read_b128 / ds_write_b128, conflict-free), not in VGPRs; only the
 // hit distance stays in a register (every box test reads it).
-template <int kStep, bool kLds>
+//
+// kW = 6: the 64-B node of bvh_build.h (at most six children; one 64-B
+// half-line per visit, four loads instead of five; same hit-bit scheme).
+template <int kStep, bool kLds, int kW = 8>
 struct Tracer8T {
+    static constexpr uint32_t kQuads = kW == 6 ? kNode6Quads : kNode8Quads;
+    // the 64-B node's visit fits 64 VGPRs: 8 waves per SIMD where the LDS
+    // stack allows it (the 80-B node's spills there)
+    static constexpr int kMinWaves = kW == 6 ? SPT_ISECT_WAVES6 : SPT_ISECT_WAVES;
     WoopRay wr;
     V3 o;
     float ix, iy, iz, tmin;
@@ -293,8 +309,74 @@ struct Tracer8T {
     }
 
     __device__ __forceinline__ void visit(const DeviceScene& sc, uint32_t node) {
-        const uint4* np = sc.nodes8 + (size_t)node * kNode8Quads;
-        visit_words(np[0], np[1], np[2], np[3], np[4]);
+        const uint4* np = sc.nodes8 + (size_t)node * kQuads;
+        if constexpr (kW == 6) visit_words6(np[0], np[1], np[2], np[3]);
+        else visit_words(np[0], np[1], np[2], np[3], np[4]);
+    }
+
+    // inner children's meta bytes 0b001_11sss (24 + slot) take the ray's
+    // octant in their low 3 bits (byte-wise, once per meta word), so every
+    // child contributes (m >> 5) << (m & 31) with no branch.  A byte is an
+    // inner child iff its bits 3 and 4 are set (leaf offsets are < 24).
+    __device__ __forceinline__ uint32_t octx(uint32_t mw) const {
+        const uint32_t t8 = mw & (mw >> 1) & 0x08080808u;  // 0x08 in inner bytes
+        return mw ^ ((t8 - (t8 >> 3)) & oct_rep);          // 0x07 & octant
+    }
+
+    __device__ __forceinline__ void take_hits(uint32_t hm, uint32_t group, uint32_t tri_base) {
+        nhits = (hm & 0xff000000u) | group;
+        if constexpr (kStep >= 2) {
+            if (thits) {  // the current group still has triangles: queue the new one
+                tbase2 = tri_base;
+                thits2 = hm & 0x00ffffffu;
+                return;
+            }
+        }
+        tbase = tri_base;
+        thits = hm & 0x00ffffffu;
+    }
+
+    // The 64-B node: q0 = (origin, tri_base), q1 = (meta 0-3, meta 4-5 | ex |
+    // ey, group | ez, lo.x 0-3), q2 = (hi.x, lo.y, hi.y, lo.z 0-3), q3 =
+    // (hi.z 0-3, then per axis lo4 lo5 hi4 hi5).
+    __device__ __forceinline__ void visit_words6(const uint4 q0, const uint4 q1, const uint4 q2, const uint4 q3) {
+        const float ax = u2f(((q1.y >> 16) & 0xffu) << 23) * ix;
+        const float ay = u2f((q1.y >> 24) << 23) * iy;
+        const float az = u2f((q1.z >> 24) << 23) * iz;
+        const float bx = (u2f(q0.x) - o.x) * ix;
+        const float by = (u2f(q0.y) - o.y) * iy;
+        const float bz = (u2f(q0.z) - o.z) * iz;
+        const float mx = (fabsf(bx) + 255.0f * fabsf(ax)) * kMarginRel;
+        const float my = (fabsf(by) + 255.0f * fabsf(ay)) * kMarginRel;
+        const float mz = (fabsf(bz) + 255.0f * fabsf(az)) * kMarginRel;
+        const float bxe = bx - mx, bxx = bx + mx, bye = by - my, byx = by + my, bze = bz - mz, bzx = bz + mz;
+        const bool px = ix >= 0.0f, py = iy >= 0.0f, pz = iz >= 0.0f;
+        const uint32_t exl = px ? q1.w : q2.x, xxl = px ? q2.x : q1.w;
+        const uint32_t eyl = py ? q2.y : q2.z, xyl = py ? q2.z : q2.y;
+        const uint32_t ezl = pz ? q2.w : q3.x, xzl = pz ? q3.x : q2.w;
+        // children 4 and 5: entry planes into bytes 0-1, exit planes into 2-3
+        const uint32_t e45x = px ? q3.y : __builtin_amdgcn_alignbit(q3.y, q3.y, 16u);
+        const uint32_t e45y = py ? q3.z : __builtin_amdgcn_alignbit(q3.z, q3.z, 16u);
+        const uint32_t e45z = pz ? q3.w : __builtin_amdgcn_alignbit(q3.w, q3.w, 16u);
+        uint32_t hm = 0;
+        const uint32_t mlo = octx(q1.x), mhi = octx(q1.y);
+#pragma unroll
+        for (uint32_t c = 0; c < 6; c++) {
+            const uint32_t sh = (c & 3u) * 8u;
+            const bool lo = c < 4;
+            const float tex = fmaf((float)(((lo ? exl : e45x) >> sh) & 0xffu), ax, bxe);
+            const float txx = fmaf((float)(((lo ? xxl : e45x) >> (lo ? sh : sh + 16u)) & 0xffu), ax, bxx);
+            const float tey = fmaf((float)(((lo ? eyl : e45y) >> sh) & 0xffu), ay, bye);
+            const float txy = fmaf((float)(((lo ? xyl : e45y) >> (lo ? sh : sh + 16u)) & 0xffu), ay, byx);
+            const float tez = fmaf((float)(((lo ? ezl : e45z) >> sh) & 0xffu), az, bze);
+            const float txz = fmaf((float)(((lo ? xzl : e45z) >> (lo ? sh : sh + 16u)) & 0xffu), az, bzx);
+            const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tmin));
+            const float tf = fminf(fminf(txx, txy), fminf(txz, h.t));
+            const uint32_t mw = lo ? mlo : mhi;
+            const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);
+            hm = (tn <= tf) ? (hm | bits) : hm;
+        }
+        take_hits(hm, q1.z & 0x00ffffffu, q0.w);
     }
 
     __device__ __forceinline__ void visit_words(const uint4 w0, const uint4 w1, const uint4 w2, const uint4 w3,
@@ -316,14 +398,6 @@ struct Tracer8T {
         const uint32_t eyl = py ? w2.z : w4.x, eyh = py ? w2.w : w4.y, xyl = py ? w4.x : w2.z, xyh = py ? w4.y : w2.w;
         const uint32_t ezl = pz ? w3.x : w4.z, ezh = pz ? w3.y : w4.w, xzl = pz ? w4.z : w3.x, xzh = pz ? w4.w : w3.y;
         uint32_t hm = 0;
-        // inner children's meta bytes 0b001_11sss (24 + slot) take the ray's
-        // octant in their low 3 bits (byte-wise, once per meta word), so every
-        // child contributes (m >> 5) << (m & 31) with no branch.  A byte is an
-        // inner child iff its bits 3 and 4 are set (leaf offsets are < 24).
-        const auto octx = [&](uint32_t mw) {
-            const uint32_t t8 = mw & (mw >> 1) & 0x08080808u;  // 0x08 in inner bytes
-            return mw ^ ((t8 - (t8 >> 3)) & oct_rep);          // 0x07 & octant
-        };
         const uint32_t mlo = octx(w1.z), mhi = octx(w1.w);
 #pragma unroll
         for (uint32_t c = 0; c < 8; c++) {
@@ -341,16 +415,7 @@ struct Tracer8T {
             const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);
             hm = (tn <= tf) ? (hm | bits) : hm;
         }
-        nhits = (hm & 0xff000000u) | (w1.x >> 3);
-        if constexpr (kStep >= 2) {
-            if (thits) {  // the current group still has triangles: queue the new one
-                tbase2 = w1.y;
-                thits2 = hm & 0x00ffffffu;
-                return;
-            }
-        }
-        tbase = w1.y;
-        thits = hm & 0x00ffffffu;
+        take_hits(hm, w1.x >> 3, w1.y);
     }
 
     __device__ __forceinline__ bool tri_test(const DeviceScene& sc, const float4 t0, const float4 t1, const float4 t2,
@@ -437,10 +502,15 @@ struct Tracer8T {
                 stats.push(spa / kRow);
             }
         }
-        const uint4* np = sc.nodes8 + (size_t)node * kNode8Quads;
-        const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3], w4 = np[4];
+        const uint4* np = sc.nodes8 + (size_t)node * kQuads;
+        const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3];
+        uint4 w4 = w3;
+        if constexpr (kW != 6) w4 = np[4];
         if (has_tri && tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
-        if (do_node) visit_words(w0, w1, w2, w3, w4);
+        if (do_node) {
+            if constexpr (kW == 6) visit_words6(w0, w1, w2, w3);
+            else visit_words(w0, w1, w2, w3, w4);
+        }
         return false;
     }
 
@@ -481,10 +551,12 @@ struct Tracer8T {
 #define SPT_LDS_RAY 1
 #endif
 using Tracer8 = Tracer8T<SPT_MERGED_STEP, SPT_LDS_RAY>;  // isect kernels
+using Tracer6 = Tracer8T<SPT_MERGED_STEP, SPT_LDS_RAY, 6>;  // isect kernels, 64-B nodes
 #ifndef SPT_FUSED_LDS
 #define SPT_FUSED_LDS 1
 #endif
 using Tracer8F = Tracer8T<SPT_FUSED_STEP, SPT_FUSED_LDS>;  // fused trace+shade kernel
+using Tracer6F = Tracer8T<SPT_FUSED_STEP, SPT_FUSED_LDS, 6>;
 
 template <typename Tr, typename Stats = NoStats>
 __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, float tmin, float tmax,
@@ -505,11 +577,8 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
 // quarter from the launch-wide counter *a.next, which evens out the tail.
 // The last cast of a path only needs a yes/no answer (a miss is the only thing
 // that contributes, main.cpp:407), so it runs as an any-hit query.
-#ifndef SPT_ISECT_WAVES
-#define SPT_ISECT_WAVES 1
-#endif
 template <typename Tr, bool kStats>
-__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_ISECT_WAVES, 8)))
+__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(kStats ? 1 : Tr::kMinWaves, 8)))
 void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
@@ -589,9 +658,9 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     const V3 d = v3(a.dx[i], a.dy[i], a.dz[i]);
     const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
     NoStats st;
-    TraceHit h = a.sc.nodes8
-                     ? trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
-                     : trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
+    TraceHit h = !a.sc.nodes8 ? trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
+                 : a.sc.node6 ? trace<Tracer6>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
+                              : trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
     if (a.sc.nsph) trace_spheres(a.sc, o, d, tmin, a.closest == 0, h);
     if (h.slot == -1) {
         a.tri_id[i] = -1;
@@ -609,12 +678,13 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
 // counter) and refilling its finished lanes from that share, so lanes do not
 // idle behind a wave's slowest ray.  Masked-off rays take a slot and write
 // nothing (wavefront_isect.cu:86).
+template <typename Tr>
 __global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_ISECT_WAVES, 8)))
 void isect_public_persistent_kernel(IsectPublicArgs a) {
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
     NoStats st;
-    Tracer8 tr;
+    Tr tr;
     uint32_t ray = 0;
     bool busy = false;
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
@@ -1246,13 +1316,36 @@ static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_it
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
-    return a.sc.nodes8 ? launch_isect_queue_t<Tracer8, false>(a, grid_items, s)
-                       : launch_isect_queue_t<Tracer, false>(a, grid_items, s);
+    if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false>(a, grid_items, s);
+    return a.sc.node6 ? launch_isect_queue_t<Tracer6, false>(a, grid_items, s)
+                      : launch_isect_queue_t<Tracer8, false>(a, grid_items, s);
 }
 
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
-    return a.sc.nodes8 ? launch_isect_queue_t<Tracer8, true>(a, grid_items, s)
-                       : launch_isect_queue_t<Tracer, true>(a, grid_items, s);
+    if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, true>(a, grid_items, s);
+    return a.sc.node6 ? launch_isect_queue_t<Tracer6, true>(a, grid_items, s)
+                      : launch_isect_queue_t<Tracer8, true>(a, grid_items, s);
+}
+
+template <typename Tr>
+static uint32_t public_persistent_blocks(size_t lds) {
+    static thread_local size_t cached_lds = 0;
+    static thread_local uint32_t cached = 0;
+    static thread_local int cached_dev = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (!cached || cached_lds != lds || cached_dev != dev) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_public_persistent_kernel<Tr>, kIsectBlock,
+                                                         lds) != hipSuccess || per_cu <= 0)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        cached = (uint32_t)(per_cu * cus);
+        cached_lds = lds;
+        cached_dev = dev;
+    }
+    return cached;
 }
 
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
@@ -1263,25 +1356,13 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
     // traces 25-30 % faster in lockstep waves; the persistent kernel wins on
     // incoherent rays (+25-36 %) — tools/isect_api_bench.py, DESIGN.md §4
     if (a.sc.nodes8 && a.persistent) {
-        static thread_local size_t cached_lds = 0;
-        static thread_local uint32_t cached = 0;
-        static thread_local int cached_dev = -1;
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (!cached || cached_lds != lds || cached_dev != dev) {
-            int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_public_persistent_kernel, kIsectBlock,
-                                                             lds) != hipSuccess || per_cu <= 0)
-                per_cu = 1;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                cus = 256;
-            cached = (uint32_t)(per_cu * cus);
-            cached_lds = lds;
-            cached_dev = dev;
-        }
+        const uint32_t cached = a.sc.node6 ? public_persistent_blocks<Tracer6>(lds) : public_persistent_blocks<Tracer8>(lds);
         // at least 64 rays per wave (a wave's share), at most the chip's occupancy
         const uint32_t blocks = max(1u, min(cached, blocks_for(a.n, kIsectBlock / 64 * 64 * 2)));
-        hipLaunchKernelGGL(isect_public_persistent_kernel, dim3(blocks), dim3(kIsectBlock), lds, s, a);
+        if (a.sc.node6)
+            hipLaunchKernelGGL(isect_public_persistent_kernel<Tracer6>, dim3(blocks), dim3(kIsectBlock), lds, s, a);
+        else
+            hipLaunchKernelGGL(isect_public_persistent_kernel<Tracer8>, dim3(blocks), dim3(kIsectBlock), lds, s, a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
@@ -1327,6 +1408,11 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
 }
 
 hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out) {
+    if (a.sc.nodes8 && a.sc.node6) {
+        if (mode == kModeEmit) return launch_fused_t<Tracer6F, kModeEmit>(a, s, lanes_out);
+        if (mode == kModeAlbedo) return launch_fused_t<Tracer6F, kModeAlbedo>(a, s, lanes_out);
+        return launch_fused_t<Tracer6F, kModeUnit>(a, s, lanes_out);
+    }
     if (a.sc.nodes8) {
         if (mode == kModeEmit) return launch_fused_t<Tracer8F, kModeEmit>(a, s, lanes_out);
         if (mode == kModeAlbedo) return launch_fused_t<Tracer8F, kModeAlbedo>(a, s, lanes_out);

@@ -10,6 +10,7 @@ namespace spt {
 
 constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kNode8Quads = 8;         // BVH8 node stride in 16-B units (80 B used, padded to one 128-B line)
+constexpr uint32_t kNode6Quads = 4;         // 64-B node (at most six children, bvh_build.h): one 64-B half-line
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 #ifndef SPT_SHADE_BLOCK
 #define SPT_SHADE_BLOCK 512
@@ -49,6 +50,7 @@ struct PathQueue {
 struct DeviceScene {
     const float4* nodes;   // BVH2: 4 per node (bvh_build.h)
     const uint4* nodes8;   // compressed BVH8: 5 per node (bvh_build.h); non-null selects it
+    uint32_t node6;        // nodes8 holds 64-B nodes (at most six children, bvh_build.h)
     const float4* tris;    // 3 per slot: v0 (w = original id bits), v1, v2
     const float4* snrm;    // 3 per slot: n0 (w = material id bits), n1, n2
     const float* tc;       // 6 per slot (u0 v0 u1 v1 u2 v2) or null

@@ -18,8 +18,12 @@ pytestmark = [pytest.mark.gpu,
 HOST, GPU = _lib.SPT_BUILD_HOST_SAH, _lib.SPT_BUILD_GPU_PLOC
 
 
-def make_scene(mesh, build):
-    s = sptamd.Scene()
+def make_scene(mesh, build, width=None):
+    cfg = None
+    if width is not None:
+        cfg = sptamd.default_config()
+        cfg.bvh_width = width
+    s = sptamd.Scene(cfg)
     s.add_arrays(mesh)
     s.commit(0, build=build)
     return s
@@ -42,7 +46,7 @@ def test_gpu_build_stats(mesh):
     assert g["builder"] == GPU and h["builder"] == HOST
     ntri = len(mesh["pos_tri"]) // 3 if np.ndim(mesh["pos_tri"]) == 1 else len(mesh["pos_tri"])
     assert g["ntri"] == h["ntri"] == ntri
-    assert g["bvh_width"] == 8 and 0 < g["nodes"] < ntri
+    assert g["bvh_width"] == sptamd.config_from_env().bvh_width and 0 < g["nodes"] < ntri
     # every leaf holds 1..3 triangles, every triangle one leaf
     assert ntri / 3 <= g["leaves"] <= ntri
     assert 1 <= g["max_depth"] <= 32
@@ -57,6 +61,32 @@ def test_gpu_build_render_bitexact(mesh, pipeline):
     ref, _ = O.OracleScene(mesh).render(O.reference_params(48, 40, 6, 6, rr_start_depth=99))
     np.testing.assert_array_equal(g, ref)
     np.testing.assert_array_equal(h, ref)
+
+
+@pytest.mark.parametrize("width", [6, 8])
+@pytest.mark.parametrize("build", [HOST, GPU])
+def test_node_formats_bitexact(mesh, width, build):
+    """Both wide-node formats (the 64-B six-wide node and the 80-B BVH8) from
+    both builders: renders through both pipelines and closest-hit records
+    bit-equal to the oracle."""
+    if os.environ.get("SPT_BVH"):
+        pytest.skip("SPT_BVH overrides the width")
+    s = make_scene(mesh, build, width)
+    st = s.backend.stats
+    assert st["bvh_width"] == width and st["builder"] == build
+    ref, _ = O.OracleScene(mesh).render(O.reference_params(40, 32, 4, 6, rr_start_depth=99))
+    for pipeline in ("wavefront", "fused"):
+        got, _ = render(s, 40, 32, 4, 6, rr_start_depth=99, pipeline=pipeline)
+        np.testing.assert_array_equal(got, ref)
+    rng = np.random.default_rng(11)
+    n = 8000
+    o = rng.uniform(-2.5, 2.5, size=(3, n)).astype(np.float32)
+    d = rng.normal(size=(3, n)).astype(np.float32)
+    tri, t, _, _ = s.backend.intersect_raw(sptamd.Ray3.make(o, d))
+    torch.cuda.synchronize()
+    rt, rtt, _, _ = O.OracleScene(mesh).intersect(o, d)
+    np.testing.assert_array_equal(tri.cpu().numpy(), rt)
+    np.testing.assert_array_equal(t.cpu().numpy()[rt >= 0], rtt[rt >= 0])
 
 
 def test_gpu_build_isect_bitexact(mesh):

@@ -189,7 +189,7 @@ def _soups():
 
 @pytest.mark.parametrize("name,tv", list(_soups()), ids=lambda x: x if isinstance(x, str) else "")
 def test_host_bvh_builders(name, tv):
-    for width, collapse in ((8, 0), (8, 1), (2, 0)):
+    for width, collapse in ((6, 0), (6, 1), (8, 0), (8, 1), (2, 0)):
         cfg = sptamd.default_config()
         cfg.bvh_width, cfg.collapse = width, collapse
         st = _lib.SceneStats()

@@ -28,6 +28,9 @@ for s in "$@"; do
     testsv) run testsv 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
     tests2) run tests2 900 env SPT_BVH=2 python -m pytest tests -m gpu -q -x ;;
+    tests8) run tests8 900 env SPT_BVH=8 python -m pytest tests -m gpu -q -x ;;
+    trav48) run trav48 600 env SPT_BVH=8 python tools/trav_stats.py --city --depths 8 --spp 8 ;;
+    trav18) run trav18 600 env SPT_BVH=8 python tools/trav_stats.py --depths 8 ;;
     testsgb) run testsgb 900 env SPT_BUILD=gpu python -m pytest tests -m gpu -q -x ;;
     bench4gq) run bench4gq 600 env SPT_BUILD=gpu python bench.py --config 4 --steps 2 --warmup 1 --no-cpu-baseline ;;
     bench1gq) run bench1gq 600 env SPT_BUILD=gpu python bench.py --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
