@@ -218,6 +218,9 @@ typedef struct spt_config {
     /* --- spt_intersect */
     uint32_t public_persistent;     /* 1: lane-refill persistent kernel, 0: one lane per ray  [0..1] */
     uint32_t public_refill_idle;    /* its refill threshold, 16                              [1..64] */
+    /* --- scene build, continued */
+    uint32_t pack_groups;           /* 1: wide-BVH child groups packed into each other's empty
+                                       slots (denser node lines), 0: eight aligned slots each [0..1] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -142,6 +142,7 @@ struct spt_scene_t {
     float4* nodes = nullptr;
     uint4* nodes8 = nullptr;
     uint32_t node6 = 0;  // nodes8 holds the 64-B six-wide nodes (spt_config.bvh_width 6)
+    uint32_t group_shift = 3;  // 0: packed child groups, 3: aligned groups of eight slots
     float4* tris = nullptr;
     float4* snrm = nullptr;
     float* tc = nullptr;
@@ -169,7 +170,7 @@ struct spt_scene_t {
 
     DeviceScene dev() const {
         DeviceScene d;
-        d.nodes = nodes; d.nodes8 = nodes8; d.node6 = node6; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
+        d.nodes = nodes; d.nodes8 = nodes8; d.node6 = node6; d.group_shift = group_shift; d.tris = tris; d.snrm = snrm; d.tc = tc; d.orig2slot = orig2slot;
         d.albedo = albedo; d.nmat = nmat; d.emission = emission; d.nemit = nemit; d.stack_depth = stack_depth; d.empty = ntri == 0;
         d.tex_info = tex_info; d.ntex = ntex; d.texels = texels;
         d.spheres = spheres; d.sph_mat = sph_mat; d.nsph = nsph;
@@ -316,6 +317,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(film_budget_bytes, 12, UINT64_MAX)
     CFG_RANGE(public_persistent, 0, 1)
     CFG_RANGE(public_refill_idle, 1, 64)
+    CFG_RANGE(pack_groups, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -356,7 +358,8 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     uint32_t nslots = 0;
     {
         uint32_t* holes = nullptr;
-        const hipError_t he = gpu_bvh8_holes(g.nodes8, g.nnodes, s, &holes, &nslots, width);
+        const hipError_t he = gpu_bvh8_holes(g.nodes8, g.nnodes, s, &holes, &nslots, width,
+                                             cfg.pack_groups ? &sc->group_shift : nullptr);
         (void)hipFree(g.nodes8);
         if (he) {
             (void)hipFree(g.slot2tri);
@@ -592,7 +595,8 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
         if (!us) us = upload(&compact, padded.data(), padded.size() * sizeof(uint32_t));
         if (!us) {
             uint32_t* holes = nullptr;
-            const hipError_t he = gpu_bvh8_holes(compact, (uint32_t)nn, nullptr, &holes, &nslots, width);
+            const hipError_t he = gpu_bvh8_holes(compact, (uint32_t)nn, nullptr, &holes, &nslots, width,
+                                                 cfg.pack_groups ? &sc->group_shift : nullptr);
             if (he) us = fail(he == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP,
                               "spt_scene_create (BVH8 layout): %s", hipGetErrorString(he));
             else { sc->nodes8 = (uint4*)holes; sc->node6 = width == 6; }
@@ -686,6 +690,7 @@ void spt_default_config(spt_config* c) {
     c->film_budget_bytes = 4ull << 30;
     c->public_persistent = 0;
     c->public_refill_idle = kRefillIdle;
+    c->pack_groups = 1;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -698,6 +703,7 @@ spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
     // the scene keeps the build it has
     sc->cfg.build = old.build; sc->cfg.bvh_width = old.bvh_width; sc->cfg.gpu_build_min_tris = old.gpu_build_min_tris;
     sc->cfg.collapse = old.collapse; sc->cfg.ploc_radius = old.ploc_radius; sc->cfg.stack_slack = old.stack_slack;
+    sc->cfg.pack_groups = old.pack_groups;
     return SPT_OK;
 }
 

@@ -33,9 +33,13 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
 // success the caller owns *out (device, *nslots nodes).  Synchronises s.
 // width 6: every node has at most six children and is re-encoded as the
 // 64-B node of bvh_build.h (kNode6Quads quads per slot); else copied as is
-// (kNode8Quads quads per slot).
+// (kNode8Quads quads per slot).  group_shift non-null: the groups are packed
+// into each other's holes (a node's group word is its first child slot,
+// *group_shift = 0) when that fits 24 bits, else aligned (group word = slot /
+// 8, *group_shift = 3); null: aligned.  Child s of a node sits at
+// (group word << shift) + s.
 hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t nnodes, hipStream_t s, uint32_t** out,
-                          uint32_t* nslots, int width = 8);
+                          uint32_t* nslots, int width = 8, uint32_t* group_shift = nullptr);
 
 }  // namespace spt
 

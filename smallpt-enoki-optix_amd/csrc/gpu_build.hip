@@ -541,15 +541,28 @@ struct Temp {
     } while (0)
 
 // Holes layout (gpu_bvh8_holes): flag nodes with inner children; their
-// exclusive scan numbers the child groups (group g -> slots 8 (g + 1) ..).
+// exclusive scan numbers the child groups g; group g's child in octant slot s
+// goes to slot (gword[g] << shift) + s — packed (shift 0: gword a slot
+// index chosen on the host so that groups fill each other's holes) or
+// aligned (shift 3: gword = g + 1, eight slots per group).
 __global__ __launch_bounds__(kBlock) void holes_flag_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
                                                             uint32_t* __restrict__ flags) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i < n) flags[i] = (nodes[(size_t)i * kNode8Quads * 4 + 3] >> 24) ? 1u : 0u;
 }
 
+__global__ __launch_bounds__(kBlock) void holes_mask_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
+                                                            const uint32_t* __restrict__ group,
+                                                            uint8_t* __restrict__ gmask) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t imask = nodes[(size_t)i * kNode8Quads * 4 + 3] >> 24;
+    if (imask) gmask[group[i]] = (uint8_t)imask;
+}
+
 __global__ __launch_bounds__(kBlock) void holes_index_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
                                                              const uint32_t* __restrict__ group,
+                                                             const uint32_t* __restrict__ gword, uint32_t shift,
                                                              uint32_t* __restrict__ newidx) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -557,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void holes_index_kernel(const uint32_t* __r
     const uint32_t* w = nodes + (size_t)i * kNode8Quads * 4;
     const uint32_t imask = w[3] >> 24;
     if (!imask) return;
-    const uint32_t base = 8u * (group[i] + 1u), first = w[4];
+    const uint32_t base = gword[group[i]] << shift, first = w[4];
     uint32_t r = 0;
     for (uint32_t s = 0; s < 8; s++)
         if ((imask >> s) & 1u) newidx[first + r++] = base + s;  // r-th inner child sits in slot s
@@ -565,6 +578,7 @@ __global__ __launch_bounds__(kBlock) void holes_index_kernel(const uint32_t* __r
 
 __global__ __launch_bounds__(kBlock) void holes_copy_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
                                                             const uint32_t* __restrict__ group,
+                                                            const uint32_t* __restrict__ gword,
                                                             const uint32_t* __restrict__ newidx,
                                                             uint32_t* __restrict__ out) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -573,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void holes_copy_kernel(const uint32_t* __re
     uint4* dst = (uint4*)(out + (size_t)newidx[i] * kNode8Quads * 4);
     for (uint32_t q = 0; q < kNode8Quads; q++) dst[q] = src[q];
     uint4 w1 = src[1];
-    w1.x = (src[0].w >> 24) ? 8u * (group[i] + 1u) : 0u;  // w4: first slot of the child group
+    w1.x = (src[0].w >> 24) ? gword[group[i]] : 0u;  // w4: the child group's word
     dst[1] = w1;
 }
 
@@ -583,6 +597,7 @@ __global__ __launch_bounds__(kBlock) void holes_copy_kernel(const uint32_t* __re
 // A node with more than six children sets *bad (the build used width 8).
 __global__ __launch_bounds__(kBlock) void holes_copy6_kernel(const uint32_t* __restrict__ nodes, uint32_t n,
                                                              const uint32_t* __restrict__ group,
+                                                             const uint32_t* __restrict__ gword,
                                                              const uint32_t* __restrict__ newidx,
                                                              uint32_t* __restrict__ out, uint32_t* __restrict__ bad) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
@@ -605,7 +620,7 @@ __global__ __launch_bounds__(kBlock) void holes_copy6_kernel(const uint32_t* __r
         c++;
     }
     const uint32_t ew = w[3];
-    const uint32_t grp = (ew >> 24) ? group[i] + 1u : 0u;  // first child slot / 8
+    const uint32_t grp = (ew >> 24) ? gword[group[i]] : 0u;  // the child group's word
     uint32_t o[16];
     o[0] = w[0]; o[1] = w[1]; o[2] = w[2];
     o[3] = w[5];
@@ -621,10 +636,44 @@ __global__ __launch_bounds__(kBlock) void holes_copy6_kernel(const uint32_t* __r
 
 }  // namespace
 
+// Packed group bases (host, first fit over a slot bitmap): each group, in
+// order, takes the lowest base >= 1 at which its occupied octant slots are
+// all free, so the slots left empty by one group's leaf children hold other
+// groups' nodes.  Returns the slot count, 0 if it would not fit 24 bits.
+static size_t pack_groups(const std::vector<uint8_t>& gmask, std::vector<uint32_t>& gword) {
+    std::vector<uint64_t> used(1, 1u);  // slot 0: the root
+    auto is_used = [&](size_t x) { return x / 64 < used.size() && ((used[x / 64] >> (x % 64)) & 1u); };
+    size_t lo = 1, end = 1;
+    gword.resize(gmask.size());
+    for (size_t g = 0; g < gmask.size(); g++) {
+        const uint32_t m = gmask[g];
+        size_t b = lo > (size_t)__builtin_ctz(m | 0x100u) ? lo - (size_t)__builtin_ctz(m | 0x100u) : 1;
+        if (b < 1) b = 1;
+        for (;; b++) {
+            bool ok = true;
+            for (uint32_t t = 0; t < 8 && ok; t++)
+                if (((m >> t) & 1u) && is_used(b + t)) ok = false;
+            if (ok) break;
+        }
+        if (b + 8 >= (1u << 24)) return 0;
+        gword[g] = (uint32_t)b;
+        for (uint32_t t = 0; t < 8; t++)
+            if ((m >> t) & 1u) {
+                const size_t x = b + t;
+                if (x / 64 >= used.size()) used.resize(x / 64 + 1, 0u);
+                used[x / 64] |= 1ull << (x % 64);
+                end = std::max(end, x + 1);
+            }
+        while (is_used(lo)) lo++;
+    }
+    return end;
+}
+
 hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, uint32_t** out, uint32_t* nslots,
-                          int width) {
+                          int width, uint32_t* group_shift) {
     *out = nullptr;
     *nslots = 0;
+    if (group_shift) *group_shift = 3;
     Temp tmp;
     uint32_t *flags, *group, *newidx, *bad;
     const uint32_t quads = width == 6 ? kNode6Quads : kNode8Quads;
@@ -648,18 +697,42 @@ hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, ui
         GB_TRY(hipStreamSynchronize(s));
         groups = last[0] + last[1];
     }
-    if (groups >= (1u << 24)) return hipErrorInvalidValue;  // w4 / 8 must fit the 24-bit stack field
-    const size_t slots = 8 * ((size_t)groups + 1);
+    // group words: packed bases when a caller takes the shift, else aligned groups
+    std::vector<uint32_t> gw(groups);
+    size_t slots = 0;
+    uint32_t shift = 3;
+    if (group_shift && groups) {
+        uint8_t* gmask = nullptr;
+        GB_TRY(tmp.get(&gmask, groups));
+        hipLaunchKernelGGL(holes_mask_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, gmask);
+        GB_TRY(hipGetLastError());
+        std::vector<uint8_t> hm(groups);
+        GB_TRY(hipMemcpyAsync(hm.data(), gmask, groups, hipMemcpyDeviceToHost, s));
+        GB_TRY(hipStreamSynchronize(s));
+        slots = pack_groups(hm, gw);
+        if (slots) shift = 0;
+    }
+    if (shift) {
+        if (groups >= (1u << 24)) return hipErrorInvalidValue;  // the group word must fit the 24-bit stack field
+        for (uint32_t g = 0; g < groups; g++) gw[g] = g + 1u;
+        slots = 8 * ((size_t)groups + 1);
+    }
+    if (slots == 0) slots = 1;
+    uint32_t* gword = nullptr;
+    GB_TRY(tmp.get(&gword, groups));
+    if (groups) GB_TRY(hipMemcpyAsync(gword, gw.data(), sizeof(uint32_t) * groups, hipMemcpyHostToDevice, s));
     uint32_t* o = nullptr;
     GB_TRY(dmalloc(&o, slots * quads * 4));
     hipError_t e = hipMemsetAsync(o, 0, slots * quads * 16, s);
     if (!e && n) {
-        hipLaunchKernelGGL(holes_index_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx);
+        hipLaunchKernelGGL(holes_index_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, gword, shift,
+                           newidx);
         if (width == 6)
-            hipLaunchKernelGGL(holes_copy6_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx, o,
-                               bad);
+            hipLaunchKernelGGL(holes_copy6_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, gword,
+                               newidx, o, bad);
         else
-            hipLaunchKernelGGL(holes_copy_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, newidx, o);
+            hipLaunchKernelGGL(holes_copy_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, d_nodes, n, group, gword,
+                               newidx, o);
         e = hipGetLastError();
     }
     if (!e) e = hipStreamSynchronize(s);
@@ -674,6 +747,7 @@ hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, ui
     }
     *out = o;
     *nslots = (uint32_t)slots;
+    if (group_shift) *group_shift = shift;
     return hipSuccess;
 }
 

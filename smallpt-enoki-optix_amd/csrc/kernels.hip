@@ -415,7 +415,7 @@ struct Tracer8T {
             const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);
             hm = (tn <= tf) ? (hm | bits) : hm;
         }
-        take_hits(hm, w1.x >> 3, w1.y);
+        take_hits(hm, w1.x, w1.y);
     }
 
     __device__ __forceinline__ bool tri_test(const DeviceScene& sc, const float4 t0, const float4 t1, const float4 t2,
@@ -491,7 +491,7 @@ struct Tracer8T {
             nhits = *stack_top(L);
         }
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits | 1u);
-        const uint32_t child = ((nhits & 0x00ffffffu) << 3) | (((bit - 24u) ^ oct_rep) & 7u);
+        const uint32_t child = ((nhits & 0x00ffffffu) << sc.group_shift) + (((bit - 24u) ^ oct_rep) & 7u);
         const uint32_t node = do_node ? child : 0u;
         if (do_node) {
             stats.node();
@@ -536,7 +536,7 @@ struct Tracer8T {
         }
         stats.node();
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits);
-        const uint32_t child = ((nhits & 0x00ffffffu) << 3) | (((bit - 24u) ^ oct_rep) & 7u);
+        const uint32_t child = ((nhits & 0x00ffffffu) << sc.group_shift) + (((bit - 24u) ^ oct_rep) & 7u);
         nhits &= ~(1u << bit);
         if (nhits & 0xff000000u) {
             *stack_top(L) = nhits;

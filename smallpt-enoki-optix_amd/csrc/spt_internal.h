@@ -51,6 +51,7 @@ struct DeviceScene {
     const float4* nodes;   // BVH2: 4 per node (bvh_build.h)
     const uint4* nodes8;   // compressed BVH8: 5 per node (bvh_build.h); non-null selects it
     uint32_t node6;        // nodes8 holds 64-B nodes (at most six children, bvh_build.h)
+    uint32_t group_shift;  // child s of a node at (group word << group_shift) + s (gpu_bvh8_holes)
     const float4* tris;    // 3 per slot: v0 (w = original id bits), v1, v2
     const float4* snrm;    // 3 per slot: n0 (w = material id bits), n1, n2
     const float* tc;       // 6 per slot (u0 v0 u1 v1 u2 v2) or null
