@@ -6,7 +6,8 @@ import subprocess
 import sys
 
 cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Icsrc",
-       "-fhip-fp32-correctly-rounded-divide-sqrt", "-Rpass-analysis=kernel-resource-usage",
+       "-fhip-fp32-correctly-rounded-divide-sqrt", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
+       "-Rpass-analysis=kernel-resource-usage",
        "-c", "csrc/kernels.hip", "-o", "/dev/null"] + sys.argv[1:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 name = None
