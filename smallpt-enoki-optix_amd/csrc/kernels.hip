@@ -17,6 +17,9 @@ namespace spt {
 #ifndef SPT_ISECT_WAVES6
 #define SPT_ISECT_WAVES6 8
 #endif
+#ifndef SPT_FUSED_WAVES
+#define SPT_FUSED_WAVES 5  // the fused kernel: 6 (80 VGPRs, no spills in unit mode) ran 2 % slower
+#endif
 
 // ------------------------------------------------------------- traversal
 // woop_test's double-precision fallback re-reads the triangle (rare path) so
@@ -1001,11 +1004,9 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 // refill_kernel) in the lanes that became free.  Path state never leaves the
 // registers, so there are no queues, compaction or per-bounce launches.  The
 // per-(sample, pixel) film writes are the same, so the image is bit-identical.
-#ifndef SPT_FUSED_WAVES
-#define SPT_FUSED_WAVES 5
-#endif
 template <typename Tr, int kMode>
-__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
+__global__ __launch_bounds__(kIsectBlock)
+__attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
     extern __shared__ uint32_t lds_stack[];
