@@ -226,9 +226,14 @@ struct NoReload {  // the vertices stay in registers (host)
 // double-precision edge fallback (an edge function exactly 0) re-derives the
 // sheared vertices from reload() — on the device a re-read of the triangle,
 // so the single-precision path does not keep them live.
+//
+// woop_test_raw stops before the barycentric divides: it returns t and the
+// edge functions V, W with det, so a caller that keeps only the closest hit
+// divides once, u = V / det and v = W / det, for the hit it keeps (the same
+// correctly rounded quotients).
 template <typename Reload>
-SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
-                      float& t_out, float& u_out, float& v_out) {
+SPT_HD bool woop_test_raw(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
+                          float& t_out, float& V_out, float& W_out, float& det_out) {
     const WoopShear w = woop_shear(r, p0, p1, p2);
     const float Akz = w.Akz, Bkz = w.Bkz, Ckz = w.Ckz;
     float U = w.Cx * w.By - w.Cy * w.Bx;
@@ -259,6 +264,17 @@ SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, floa
     float t = T / det;
     if (!(t >= tmin && t <= tmax)) return false;
     t_out = t;
+    V_out = V;
+    W_out = W;
+    det_out = det;
+    return true;
+}
+
+template <typename Reload>
+SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
+                      float& t_out, float& u_out, float& v_out) {
+    float V, W, det;
+    if (!woop_test_raw(r, p0, p1, p2, reload, tmin, tmax, t_out, V, W, det)) return false;
     u_out = V / det;
     v_out = W / det;
     return true;
