@@ -37,7 +37,7 @@ FUSED_BYTES_PER_PATH = 12      # per-sample film RGB write
 CONFIGS = {
     0: dict(scene="mitsuba_synth", width=256, height=256, spp=4, depth=4, smallpt=False),
     1: dict(scene="mitsuba_synth", width=1024, height=1024, spp=64, depth=8, smallpt=False),
-    2: dict(scene="cornell_spheres", width=1024, height=1024, spp=1024, depth=10, smallpt=True),
+    2: dict(scene="smallpt_analytic", width=1024, height=1024, spp=1024, depth=10, smallpt=True),
     3: dict(scene="mitsuba_synth", width=4096, height=4096, spp=256, depth=8, smallpt=False),
     4: dict(scene="city_synth", width=1920, height=1080, spp=64, depth=8, smallpt=False),
 }
@@ -50,8 +50,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=1, choices=sorted(CONFIGS),
                     help="BASELINE.json configs[i]: 0 mitsuba 256^2x4 depth 4 (plumbing), 1 mitsuba 1024^2x64 "
-                         "(headline), 2 Cornell 1024^2x1024 "
-                         "(emitters, albedo, roulette), 3 mitsuba 4096^2x256, 4 10M-tri city 1920x1080x64")
+                         "(headline), 2 smallpt's Cornell box 1024^2x1024 (analytic mirror / glass / light spheres, "
+                         "emitters, albedo, roulette; --scene cornell_spheres: tessellated diffuse spheres), "
+                         "3 mitsuba 4096^2x256, 4 10M-tri city 1920x1080x64")
     ap.add_argument("--width", type=int, default=0)
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--spp", type=int, default=0)
@@ -86,7 +87,10 @@ def workload(args, scenes):
     sky 1, main.cpp:383 camera)."""
     if args.scene == "city_synth":  # 10M triangles through the pbrt-v3 reader (San Miguel's format), PLY meshes
         return scenes.scene_pbrt("city_synth"), {}, None, None
-    src = scenes.scene_obj(args.scene)
+    if args.scene == "smallpt_analytic":  # smallpt's own scene: quads for the walls, analytic mirror / glass / light spheres
+        src = scenes.smallpt_analytic()
+    else:
+        src = scenes.scene_obj(args.scene)
     if not args.smallpt:
         return src, {}, None, None
     kw = dict(camera=scenes.cornell_camera(), rr_start_depth=5, env=(0.0, 0.0, 0.0))

@@ -40,6 +40,7 @@ for s in "$@"; do
     bench2q|bench3q|bench4q) c=${s#bench}; run $s 600 python bench.py --config ${c%q} --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchwf) for wf in ${WFS:-1048576 4194304 8388608}; do run benchwf$wf 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --wavefront $wf; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    prof2s) run prof2s 600 env SPT_STREAMS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof2s -o run --output-format csv -- python bench.py --config 2 --steps 1 --warmup 1 --no-cpu-baseline ;;
     prof2|prof4) run $s 600 rocprofv3 --kernel-trace --stats -d gpurun_out/$s -o run --output-format csv -- python bench.py --config ${s#prof} --steps 1 --warmup 1 --no-cpu-baseline ;;
     pmcfetch) run pmcfetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmcwrite) run pmcwrite 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex isect_queue -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
