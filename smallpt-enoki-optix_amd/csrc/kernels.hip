@@ -688,6 +688,8 @@ void isect_queue_kernel(IsectQueueArgs a) {
 }
 
 // __raygen__rg (wavefront_isect.cu:80-112) semantics for the public C ABI.
+// One instance per node format, so each keeps only its own tracer's registers.
+template <typename Tr>
 __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicArgs a) {
     extern __shared__ uint32_t lds_stack[];
     const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
@@ -698,9 +700,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
     const V3 d = v3(a.dx[i], a.dy[i], a.dz[i]);
     const float tmin = a.tmin ? a.tmin[i] : kRayTmin, tmax = a.tmax ? a.tmax[i] : kRayTmax;
     NoStats st;
-    TraceHit h = !a.sc.nodes8 ? trace<Tracer>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
-                 : a.sc.node6 ? trace<Tracer6>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st)
-                              : trace<Tracer8>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
+    TraceHit h = trace<Tr>(a.sc, o, d, tmin, tmax, a.closest == 0, block_lds(lds_stack), st);
     if (a.sc.nsph) trace_spheres(a.sc, o, d, tmin, a.closest == 0, h);
     if (h.slot == -1) {
         a.tri_id[i] = -1;
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(kIsectBlock) void isect_public_kernel(IsectPublicAr
 // idle behind a wave's slowest ray.  Masked-off rays take a slot and write
 // nothing (wavefront_isect.cu:86).
 template <typename Tr>
-__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(SPT_ISECT_WAVES, 8)))
+__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(Tr::kMinWaves, 8)))
 void isect_public_persistent_kernel(IsectPublicArgs a) {
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
@@ -1403,7 +1403,10 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s) {
             hipLaunchKernelGGL(isect_public_persistent_kernel<Tracer8>, dim3(blocks), dim3(kIsectBlock), lds, s, a);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(isect_public_kernel, dim3(blocks_for(a.n, kIsectBlock)), dim3(kIsectBlock), lds, s, a);
+    const dim3 g(blocks_for(a.n, kIsectBlock)), b(kIsectBlock);
+    if (!a.sc.nodes8) hipLaunchKernelGGL(isect_public_kernel<Tracer>, g, b, lds, s, a);
+    else if (a.sc.node6) hipLaunchKernelGGL(isect_public_kernel<Tracer6>, g, b, lds, s, a);
+    else hipLaunchKernelGGL(isect_public_kernel<Tracer8>, g, b, lds, s, a);
     return hipGetLastError();
 }
 
