@@ -44,7 +44,7 @@ struct Collapser {
     // = the left child's share of i slots in the best distribution.
     std::vector<double> cost, dist;
     std::vector<uint8_t> take, split;
-    double c_node = 1.0, c_prim = 0.3;
+    double c_node = 1.0, c_prim = SPT_C_PRIM;
     int width = 8;                         // children per node: 8, or 6 for the 64-B device node
 
     uint32_t count_tris(int32_t code) {

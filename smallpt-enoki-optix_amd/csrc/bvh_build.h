@@ -15,6 +15,15 @@
 namespace spt {
 
 constexpr uint32_t kMaxLeafSize = 8;    // 3 count bits in the leaf code
+// SAH cost of one triangle test relative to one wide-node visit in the
+// collapse's dynamic program.  Ylitie et al. 2017 use 0.3; here a triangle
+// test is ~120 VALU against ~185 for a six-child visit, and 1.0 (smaller
+// leaves: 2.20 instead of 2.47 tests and 7.60 instead of 7.70 visits per ray)
+// measured +1.8 % on config 1 and neutral on configs 2 and 4 (0.15 / 0.6 /
+// 1.5 / 2.5: profiles/r02_v6/cprim_ab.log).
+#ifndef SPT_C_PRIM
+#define SPT_C_PRIM 1.0
+#endif
 constexpr uint32_t kMaxTriangles = 1u << 28;
 
 struct BvhBuildResult {

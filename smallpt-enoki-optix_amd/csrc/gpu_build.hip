@@ -20,6 +20,7 @@
 #include <utility>
 #include <vector>
 
+#include "bvh_build.h"
 #include "gpu_build.h"
 #include "spt_internal.h"
 
@@ -243,7 +244,7 @@ struct DpNode {
     uint32_t split;
     uint32_t take;
 };
-constexpr float kCNode = 1.0f, kCPrim = 0.3f;
+constexpr float kCNode = 1.0f, kCPrim = (float)SPT_C_PRIM;
 
 __device__ __forceinline__ float dp_kid_cost(const DpNode* __restrict__ dp, const float4* __restrict__ lo,
                                              const float4* __restrict__ hi, uint32_t ntri, uint32_t k, int i) {
