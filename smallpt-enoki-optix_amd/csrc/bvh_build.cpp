@@ -10,7 +10,12 @@
 namespace spt {
 namespace {
 
-constexpr int kBins = 32;
+// 64 / 256 bins lower config 1's BVH2 SAH by up to 2 % yet render 0.5-1.2 % slower
+// (profiles/r02_v6/sah_bins_ab.log); an exact sweep below 256 triangles changes nothing
+#ifndef SPT_SAH_BINS
+#define SPT_SAH_BINS 32
+#endif
+constexpr int kBins = SPT_SAH_BINS;
 constexpr uint32_t kSahDepthLimit = 48;  // below this depth: object-median splits
 constexpr float kNodeCost = 1.0f;
 constexpr float kTriCost = 1.0f;
