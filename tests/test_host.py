@@ -162,6 +162,7 @@ def test_config_defaults_and_env_overrides():
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
     assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 24      # spt.h docs = code
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
+    assert c.pack_groups == 1
     e = sptamd.config_from_env(environ={"SPT_STREAMS": "2", "SPT_BUILD": "gpu", "SPT_FUSED": "0",
                                         "SPT_FILM_BUDGET": "1000", "SPT_COLLAPSE": "greedy", "SPT_BVH": "2"})
     assert (e.streams, e.build, e.pipeline, e.film_budget_bytes, e.collapse, e.bvh_width) == (2, 2, 1, 1000, 1, 2)
@@ -170,7 +171,8 @@ def test_config_defaults_and_env_overrides():
 
 
 @pytest.mark.parametrize("field,value", [("streams", 0), ("streams", 5), ("bvh_width", 4), ("ploc_radius", 12),
-                                         ("isect_refill_idle", 65), ("film_budget_bytes", 0), ("pipeline", 3)])
+                                         ("isect_refill_idle", 65), ("film_budget_bytes", 0), ("pipeline", 3),
+                                         ("bvh_width", 7), ("pack_groups", 2)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)
