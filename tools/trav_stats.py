@@ -34,6 +34,11 @@ def main():
         sc.add_triangle_mesh(scenes.scene_pbrt("city_synth"))
         kw["camera"] = sc.pbrt_info["camera"]
         W, H = 1920, 1080
+    elif a.scene == "smallpt_analytic":  # BASELINE config 2: smallpt's scene, Cornell camera, smallpt materials
+        m = scenes.smallpt_analytic()
+        m["albedo"], m["emission"] = scenes.smallpt_materials(m)
+        sc.add_arrays(m)
+        kw.update(camera=scenes.cornell_camera(), rr_start_depth=5, env=(0.0, 0.0, 0.0))
     else:
         sc.add_triangle_mesh(scenes.scene_obj(a.scene))
     sc.commit(0)
