@@ -65,7 +65,7 @@ PathQueue carve_queue(char* base, size_t stride, uint32_t planes) {
     q.q1 = f4;
     q.q2 = f4 + stride;
     q.q0 = planes > 2 ? f4 + 2 * stride : nullptr;
-    q.rad = planes > 3 ? f4 + 3 * stride : nullptr;
+    q.rad = planes > 3 ? (float2*)(f4 + 3 * stride) : nullptr;  // 8 B per path (16 allocated)
     return q;
 }
 

@@ -803,8 +803,8 @@ __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o,
                                            float tr, float tg, float tb, float lr, float lg, float lb) {
     q.q1[j] = make_float4(o.x, o.y, o.z, u2f(meta));
     q.q2[j] = make_float4(d.x, d.y, d.z, u2f(pix));
-    if (kMode >= kModeAlbedo) q.q0[j] = make_float4(tr, tg, tb, 0.0f);
-    if (kMode == kModeEmit) q.rad[j] = make_float4(lr, lg, lb, 0.0f);
+    if (kMode >= kModeAlbedo) q.q0[j] = make_float4(tr, tg, tb, kMode == kModeEmit ? lr : 0.0f);
+    if (kMode == kModeEmit) q.rad[j] = make_float2(lg, lb);
 }
 
 // PCG32 of global pixel gpix (main.cpp:376) advanced past the draws a path
@@ -908,8 +908,12 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             slot = h.slot;
             hit = make_float4(u2f((uint32_t)slot), h.t, h.u, h.v);
         }
-        if (kMode >= kModeAlbedo) { const float4 q0 = a.in.q0[i]; tr = q0.x; tg = q0.y; tb = q0.z; }
-        if (kMode == kModeEmit) { const float4 l = a.in.rad[i]; lr = l.x; lg = l.y; lb = l.z; }
+        if (kMode >= kModeAlbedo) {
+            const float4 q0 = a.in.q0[i];
+            tr = q0.x; tg = q0.y; tb = q0.z;
+            if (kMode == kModeEmit) lr = q0.w;
+        }
+        if (kMode == kModeEmit) { const float2 l = a.in.rad[i]; lg = l.x; lb = l.y; }
         bool term = true, escaped = false;
         if (slot == -1) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)

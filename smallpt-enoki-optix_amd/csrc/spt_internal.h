@@ -27,7 +27,7 @@ constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lane
 enum PathMode : int {
     kModeUnit = 0,    // q1, q2                  (32 B / path); film: one byte per (sample, pixel)
     kModeAlbedo = 1,  // + q0 throughput          (48 B / path); film: RGB floats per (sample, pixel)
-    kModeEmit = 2     // + rad gathered radiance  (64 B / path); film: RGB floats
+    kModeEmit = 2     // + rad gathered radiance  (56 B / path); film: RGB floats
 };
 SPT_HD uint32_t mode_planes(int mode) { return mode == kModeUnit ? 2u : mode == kModeAlbedo ? 3u : 4u; }
 SPT_HD uint32_t mode_film_bytes(int mode) { return mode == kModeUnit ? 1u : 12u; }
@@ -37,13 +37,14 @@ SPT_HD uint32_t mode_film_bytes(int mode) { return mode == kModeUnit ? 1u : 12u;
 // each) instead of one 4-B plane per field:
 //   q1 = (o.x, o.y, o.z, meta)    origin, sample << 8 | cast    [isect, shade]
 //   q2 = (d.x, d.y, d.z, pix)     direction, tile-local pixel   [isect, shade]
-//   q0 = (tr, tg, tb, -)          throughput                    [shade; albedo / emit modes]
-//   rad = (lr, lg, lb, -)         radiance gathered so far      [shade; emit mode]
+//   q0 = (tr, tg, tb, lr)         throughput (+ red radiance)   [shade; albedo / emit modes]
+//   rad = (lg, lb)                radiance gathered so far      [shade; emit mode; 8-B plane]
 // The PCG32 state is not stored: (pixel, sample, cast) fix how many draws the
 // path has consumed, s * (4 + 2D) + 4 + 2 * cast (main.cpp:395,396,413), so
 // shade re-derives it with two jump-ahead applications.
 struct PathQueue {
-    float4 *q1, *q2, *q0, *rad;
+    float4 *q1, *q2, *q0;
+    float2* rad;
 };
 
 // Geometry on device, leaf ("slot") order.
