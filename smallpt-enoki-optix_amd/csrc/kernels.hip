@@ -228,6 +228,9 @@ constexpr float kMarginRel = 1e-6f;
 #ifndef SPT_FUSED_STEP
 #define SPT_FUSED_STEP 2
 #endif
+#ifndef SPT_EARLY_DONE
+#define SPT_EARLY_DONE 1
+#endif
 constexpr float kMinDir = 1e-20f;
 
 // kLds: the per-ray Woop constants (Sx, Sy, Sz, axis indices) and the hit
@@ -551,6 +554,12 @@ struct Tracer8T {
             if constexpr (kW == 6) visit_words6(w0, w1, w2, w3);
             else visit_words(w0, w1, w2, w3, w4);
         }
+#if SPT_EARLY_DONE
+        // nothing left (no triangles, no hit children, empty stack): finish
+        // now rather than in a step of its own, so the lane is idle (and can
+        // be refilled) one step sooner
+        if (!(thits | thits2 | (nhits & 0xff000000u)) && spa < kRow) { done = true; return true; }
+#endif
         return false;
     }
 
