@@ -18,6 +18,7 @@ The result is merged into OUT_JSON under KEY (e.g. "config1"); bench.py reads
 profiles/isect_pmc.json#config<N> for roofline.traffic and roofline.valu.
 """
 import csv
+import gzip
 import json
 import os
 import sys
@@ -27,7 +28,8 @@ from collections import defaultdict
 def passes(paths, kernel="isect_queue"):
     per = defaultdict(dict)  # counter -> {dispatch: value}
     for path in paths:
-        for r in csv.DictReader(open(path)):
+        fh = gzip.open(path, "rt") if path.endswith(".gz") else open(path)  # committed passes are gzipped
+        for r in csv.DictReader(fh):
             if kernel not in r["Kernel_Name"]:
                 continue
             d = per[r["Counter_Name"]]
