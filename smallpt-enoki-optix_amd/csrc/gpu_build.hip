@@ -638,34 +638,38 @@ __global__ __launch_bounds__(kBlock) void holes_copy6_kernel(const uint32_t* __r
 }  // namespace
 
 // Packed group bases (host, first fit over a slot bitmap): each group, in
-// order, takes the lowest base >= 1 at which its occupied octant slots are
-// all free, so the slots left empty by one group's leaf children hold other
-// groups' nodes.  Returns the slot count, 0 if it would not fit 24 bits.
+// order, takes the lowest base at which its occupied octant slots are all
+// free, so the slots left empty by one group's leaf children hold other
+// groups' nodes.  The search starts no further back than kPackWindow slots
+// behind the packed end (holes older than that are given up), so it is
+// linear in the group count.  Returns the slot count, 0 if it would not fit
+// 24 bits.
+constexpr size_t kPackWindow = 64;
 static size_t pack_groups(const std::vector<uint8_t>& gmask, std::vector<uint32_t>& gword) {
-    std::vector<uint64_t> used(1, 1u);  // slot 0: the root
-    auto is_used = [&](size_t x) { return x / 64 < used.size() && ((used[x / 64] >> (x % 64)) & 1u); };
+    std::vector<uint64_t> used(2, 0u);
+    used[0] = 1u;  // slot 0: the root
+    const auto window = [&](size_t x) -> uint32_t {  // used bits of slots x .. x + 7
+        const size_t w = x / 64, o = x % 64;
+        uint64_t v = used[w] >> o;
+        if (o) v |= used[w + 1] << (64 - o);
+        return (uint32_t)(v & 0xffu);
+    };
     size_t lo = 1, end = 1;
     gword.resize(gmask.size());
     for (size_t g = 0; g < gmask.size(); g++) {
         const uint32_t m = gmask[g];
-        size_t b = lo > (size_t)__builtin_ctz(m | 0x100u) ? lo - (size_t)__builtin_ctz(m | 0x100u) : 1;
-        if (b < 1) b = 1;
-        for (;; b++) {
-            bool ok = true;
-            for (uint32_t t = 0; t < 8 && ok; t++)
-                if (((m >> t) & 1u) && is_used(b + t)) ok = false;
-            if (ok) break;
-        }
+        if (end > lo + kPackWindow) lo = end - kPackWindow;  // give up the old holes
+        while (window(lo) & 1u) lo++;
+        const size_t c = (size_t)__builtin_ctz(m | 0x100u);
+        size_t b = lo > c ? lo - c : 1;
+        while (window(b) & m) b++;
         if (b + 8 >= (1u << 24)) return 0;
         gword[g] = (uint32_t)b;
-        for (uint32_t t = 0; t < 8; t++)
-            if ((m >> t) & 1u) {
-                const size_t x = b + t;
-                if (x / 64 >= used.size()) used.resize(x / 64 + 1, 0u);
-                used[x / 64] |= 1ull << (x % 64);
-                end = std::max(end, x + 1);
-            }
-        while (is_used(lo)) lo++;
+        if ((b + 8) / 64 + 2 > used.size()) used.resize((b + 8) / 64 + 2, 0u);
+        const size_t w = b / 64, o = b % 64;
+        used[w] |= (uint64_t)m << o;
+        if (o > 56) used[w + 1] |= (uint64_t)m >> (64 - o);
+        end = std::max(end, b + 8 - (size_t)__builtin_clz(m) + 24);  // one past the highest occupied slot
     }
     return end;
 }

@@ -74,13 +74,15 @@ __device__ __forceinline__ void trace_spheres(const DeviceScene& sc, V3 o, V3 d,
 }
 
 struct NoStats {
+    __device__ void empty_visit() {}
     __device__ void node() {}
     __device__ void tri() {}
     __device__ void step() {}
     __device__ void push(uint32_t) {}
 };
 struct TravStats {
-    uint32_t nodes = 0, tris = 0, steps = 0, max_sp = 0;
+    uint32_t nodes = 0, tris = 0, steps = 0, max_sp = 0, empties = 0;
+    __device__ void empty_visit() { empties++; }
     __device__ void node() { nodes++; }
     __device__ void tri() { tris++; }
     __device__ void step() { steps++; }
@@ -551,8 +553,10 @@ struct Tracer8T {
         if constexpr (kW != 6) w4 = np[4];
         if (has_tri && tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
         if (do_node) {
+            const uint32_t tb = thits | thits2;
             if constexpr (kW == 6) visit_words6(w0, w1, w2, w3);
             else visit_words(w0, w1, w2, w3, w4);
+            if (!(nhits & 0xff000000u) && (thits | thits2) == tb) stats.empty_visit();  // no child box hit
         }
 #if SPT_EARLY_DONE
         // nothing left (no triangles, no hit children, empty stack): finish
@@ -692,7 +696,11 @@ void isect_queue_kernel(IsectQueueArgs a) {
         atomicAdd(&a.trav_stats[1], (unsigned long long)st.tris);
         atomicAdd(&a.trav_stats[2], (unsigned long long)st.steps);
         if ((threadIdx.x & 63u) == 0) atomicAdd(&a.trav_stats[3], (unsigned long long)wave_steps);
+#if SPT_EMPTY_VISIT_STAT
+        atomicAdd(&a.trav_stats[4], (unsigned long long)st.empties);  // experiment: visits with no child hit
+#else
         atomicMax(&a.trav_stats[4], (unsigned long long)st.max_sp);
+#endif
     }
 }
 
