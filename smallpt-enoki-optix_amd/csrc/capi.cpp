@@ -378,7 +378,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
                     hipGetErrorString(e));
     };
     hipError_t e = hipSuccess;
-    if (!e) e = hipMalloc((void**)&sc->tris, sizeof(float4) * 3 * std::max<uint64_t>(ntri, 1));
+    if (!e) e = hipMalloc((void**)&sc->tris, sizeof(float4) * kTriQuads * std::max<uint64_t>(ntri, 1));
     if (!e) e = hipMalloc((void**)&sc->snrm, sizeof(float4) * 3 * std::max<uint64_t>(ntri, 1));
     if (!e && with_tc) e = hipMalloc((void**)&sc->tc, sizeof(float) * 6 * ntri);
     if (!e) e = hipMalloc((void**)&sc->orig2slot, sizeof(int32_t) * std::max<uint64_t>(ntri, 1));
@@ -546,7 +546,7 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
     const double t1 = now_ms();
 
     // Slot-ordered device arrays.
-    std::vector<float4> h_tris((size_t)ntri * 3), h_snrm((size_t)ntri * 3);
+    std::vector<float4> h_tris((size_t)ntri * kTriQuads), h_snrm((size_t)ntri * 3);
     std::vector<float> h_tc(tc_tri && tc ? (size_t)ntri * 6 : 0);
     std::vector<int32_t> h_o2s((size_t)ntri);
     for (uint64_t s = 0; s < ntri; s++) {
@@ -556,7 +556,7 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
         for (int k = 0; k < 3; k++) {
             float w = 0.0f;
             if (k == 0) { uint32_t id = t; std::memcpy(&w, &id, 4); }
-            h_tris[s * 3 + k] = make_float4(v[k * 3], v[k * 3 + 1], v[k * 3 + 2], w);
+            h_tris[s * kTriQuads + k] = make_float4(v[k * 3], v[k * 3 + 1], v[k * 3 + 2], w);
         }
         // Geometric normal fallback for a missing vertex normal (index -1).
         V3 g = normalize(cross(v3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), v3(v[6] - v[0], v[7] - v[1], v[8] - v[2])));

@@ -191,9 +191,9 @@ struct Tracer {
         for (uint32_t i = 0; i < cnt; i++) {
             stats.tri();
             const uint32_t s = first + i;
-            const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
+            const float4 t0 = sc.tris[(size_t)s * kTriQuads], t1 = sc.tris[(size_t)s * kTriQuads + 1], t2 = sc.tris[(size_t)s * kTriQuads + 2];
             float t, u, v;
-            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
+            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, u, v)) {
                 const uint32_t id = f2u(t0.w);
                 if (t < h.t || id < h.id) {
                     h.t = t;
@@ -292,7 +292,7 @@ struct Tracer8T {
         } else if (r.x == 0xffffffffu) {
             x.id = 0xffffffffu; x.u = 0.0f; x.v = 0.0f;
         } else {
-            x.id = f2u(sc.tris[(size_t)r.x * 3].w);
+            x.id = f2u(sc.tris[(size_t)r.x * kTriQuads].w);
             x.u = u2f(r.y) / u2f(r.w);
             x.v = u2f(r.z) / u2f(r.w);
         }
@@ -451,7 +451,7 @@ struct Tracer8T {
             wl.o = o; wl.Sx = u2f(wk.x); wl.Sy = u2f(wk.y); wl.Sz = u2f(wk.z); wl.k = wk.w;
             if constexpr (!kDefer) {
                 if (woop_test(wl, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                              TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
+                              TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, u, v)) {
                     // accepted means t <= h.t; a tie goes to the smaller original id
                     const uint32_t id = f2u(t0.w);
                     uint4* hr = hrec(sc, L);
@@ -465,14 +465,14 @@ struct Tracer8T {
             }
             float V, W, det;
             if (woop_test_raw(wl, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                              TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, V, W, det)) {
+                              TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, V, W, det)) {
                 // accepted means t <= h.t; a tie goes to the smaller original
                 // id (the kept hit's id read back from its triangle: rare)
                 uint4* hr = hrec(sc, L);
                 bool take = t < h.t;
                 if (!take) {
                     const uint32_t cs = hr->x;
-                    take = cs == 0xffffffffu || f2u(t0.w) < f2u(sc.tris[(size_t)cs * 3].w);
+                    take = cs == 0xffffffffu || f2u(t0.w) < f2u(sc.tris[(size_t)cs * kTriQuads].w);
                 }
                 if (take) {
                     h.t = t;
@@ -483,7 +483,7 @@ struct Tracer8T {
             return false;
         }
         if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                      TriReload{sc.tris + (size_t)s * 3}, tmin, h.t, t, u, v)) {
+                      TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, u, v)) {
             const uint32_t id = f2u(t0.w);
             if (t < h.t || id < h.id) {
                 h.t = t;
@@ -528,7 +528,7 @@ struct Tracer8T {
         const uint32_t s = has_tri ? tbase + (uint32_t)__builtin_ctz(thits) : 0u;
         if (has_tri) stats.tri();
         thits &= thits - 1u;
-        const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
+        const float4 t0 = sc.tris[(size_t)s * kTriQuads], t1 = sc.tris[(size_t)s * kTriQuads + 1], t2 = sc.tris[(size_t)s * kTriQuads + 2];
         uint4 wk = make_uint4(0u, 0u, 0u, 0u);
         if constexpr (kLds) wk = *wrec(sc, L);
         if (do_node && !(nhits & 0xff000000u)) {
@@ -574,7 +574,7 @@ struct Tracer8T {
             stats.tri();
             const uint32_t s = tbase + (uint32_t)__builtin_ctz(thits);
             thits &= thits - 1u;
-            const float4 t0 = sc.tris[(size_t)s * 3], t1 = sc.tris[(size_t)s * 3 + 1], t2 = sc.tris[(size_t)s * 3 + 2];
+            const float4 t0 = sc.tris[(size_t)s * kTriQuads], t1 = sc.tris[(size_t)s * kTriQuads + 1], t2 = sc.tris[(size_t)s * kTriQuads + 2];
             uint4 wk = make_uint4(0u, 0u, 0u, 0u);
             if constexpr (kLds) wk = *wrec(sc, L);
             if (tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
@@ -1311,8 +1311,8 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
     if (a.py) a.py[i] = a.oy[i] + t * a.dy[i];
     if (a.pz) a.pz[i] = a.oz[i] + t * a.dz[i];
     if (a.gnx || a.gny || a.gnz) {
-        const float4 p0 = a.sc.tris[(size_t)slot * 3], p1 = a.sc.tris[(size_t)slot * 3 + 1],
-                     p2 = a.sc.tris[(size_t)slot * 3 + 2];
+        const float4 p0 = a.sc.tris[(size_t)slot * kTriQuads], p1 = a.sc.tris[(size_t)slot * kTriQuads + 1],
+                     p2 = a.sc.tris[(size_t)slot * kTriQuads + 2];
         const V3 g = normalize(cross(v3(p1.x - p0.x, p1.y - p0.y, p1.z - p0.z),  // add_math.h:9-16
                                      v3(p2.x - p0.x, p2.y - p0.y, p2.z - p0.z)));
         if (a.gnx) a.gnx[i] = g.x;

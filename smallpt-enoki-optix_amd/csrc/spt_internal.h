@@ -10,6 +10,10 @@ namespace spt {
 
 constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kNode8Quads = 8;         // BVH8 node stride in 16-B units (80 B used, padded to one 128-B line)
+#ifndef SPT_TRI_QUADS
+#define SPT_TRI_QUADS 3
+#endif
+constexpr uint32_t kTriQuads = SPT_TRI_QUADS;  // triangle record stride in 16-B units (3 used: v0 + id, v1, v2)
 constexpr uint32_t kNode6Quads = 4;         // 64-B node (at most six children, bvh_build.h): one 64-B half-line
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 #ifndef SPT_SHADE_BLOCK
