@@ -18,14 +18,16 @@ pytestmark = [pytest.mark.gpu,
 HOST, GPU = _lib.SPT_BUILD_HOST_SAH, _lib.SPT_BUILD_GPU_PLOC
 
 
-def make_scene(mesh, build, width=None, pack=None):
+def make_scene(mesh, build, width=None, pack=None, collapse=None):
     cfg = None
-    if width is not None or pack is not None:
+    if width is not None or pack is not None or collapse is not None:
         cfg = sptamd.default_config()
         if width is not None:
             cfg.bvh_width = width
         if pack is not None:
             cfg.pack_groups = pack
+        if collapse is not None:
+            cfg.collapse = collapse
     s = sptamd.Scene(cfg)
     s.add_arrays(mesh)
     s.commit(0, build=build)
@@ -66,21 +68,21 @@ def test_gpu_build_render_bitexact(mesh, pipeline):
     np.testing.assert_array_equal(h, ref)
 
 
-@pytest.mark.parametrize("pack", [1, 0])
+@pytest.mark.parametrize("pack,collapse", [(1, 0), (0, 0), (1, 1)])
 @pytest.mark.parametrize("width", [6, 8])
 @pytest.mark.parametrize("build", [HOST, GPU])
-def test_node_formats_bitexact(mesh, width, build, pack):
+def test_node_formats_bitexact(mesh, width, build, pack, collapse):
     """Both wide-node formats (the 64-B six-wide node and the 80-B BVH8) from
     both builders, with child groups packed into each other's holes or
-    aligned: renders through both pipelines and closest-hit records bit-equal
+    aligned, SAH-optimal or greedy collapse: renders through both pipelines and closest-hit records bit-equal
     to the oracle; packing never grows the node array."""
     if os.environ.get("SPT_BVH") or os.environ.get("SPT_PACK"):
         pytest.skip("SPT_BVH / SPT_PACK override the layout")
-    s = make_scene(mesh, build, width, pack)
+    s = make_scene(mesh, build, width, pack, collapse)
     st = s.backend.stats
     assert st["bvh_width"] == width and st["builder"] == build
     if pack:
-        aligned = make_scene(mesh, build, width, 0).backend.stats
+        aligned = make_scene(mesh, build, width, 0, collapse).backend.stats
         assert st["device_bytes"] < aligned["device_bytes"]
     ref, _ = O.OracleScene(mesh).render(O.reference_params(40, 32, 4, 6, rr_start_depth=99))
     for pipeline in ("wavefront", "fused"):
