@@ -43,7 +43,8 @@ BvhBuildResult build_bvh(const float* tri_verts, uint64_t ntri, uint32_t max_lea
 //   w0-2  p.xyz        quantisation origin (f32)
 //   w3    ex | ey<<8 | ez<<16 | imask<<24   (biased exponents; imask: inner slots)
 //   w4    child_base   first inner child (inner children are contiguous, slot order);
-//                      on the device (gpu_bvh8_holes) child s sits at w4 + s, w4 % 8 == 0
+//                      on the device (gpu_bvh8_holes) w4 is the child-group word and
+//                      child s sits at (w4 << group_shift) + s
 //   w5    tri_base     first triangle slot of this node's leaves (contiguous)
 //   w6-7  meta[8]      0 empty; inner 0b001_(24+s); leaf unary(count)<<5 | offset
 //   w8-9  qlo.x[8]  w10-11 qlo.y[8]  w12-13 qlo.z[8]
@@ -67,7 +68,7 @@ Bvh8BuildResult build_bvh8(const float* tri_verts, uint64_t ntri, bool greedy = 
 //   w3    tri_base
 //   w4    meta[0..3]   (as above: inner 0b001_(24+s) with s its octant slot)
 //   w5    meta[4] | meta[5]<<8 | ex<<16 | ey<<24
-//   w6    group | ez<<24    group = first child slot / 8 (child s at 8 * group + s)
+//   w6    group | ez<<24    group word (child s at (group << group_shift) + s)
 //   w7-12 qlo.x qhi.x qlo.y qhi.y qlo.z qhi.z of children 0..3 (one byte each)
 //   w13-15 per axis x, y, z: lo4 | lo5<<8 | hi4<<16 | hi5<<24
 

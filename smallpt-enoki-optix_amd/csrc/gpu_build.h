@@ -26,10 +26,11 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
 
 // Re-lays a compact BVH8 (both builders' output: nnodes nodes of kNode8Quads
 // quads, the inner children of a node contiguous from w4 in slot order) so
-// that every child sits at w4 + slot: 8 slots per node that has inner
-// children, w4 a multiple of 8, the slots of leaf and empty children unused
-// ("holes").  The traversal then finds a child without a popcount and keeps
-// one word per stack entry (hit bits + w4 / 8).  Root stays at slot 0.  On
+// that every child sits at a fixed offset from its group: child s of a node
+// at (group word << shift) + s, the slots of leaf and empty children left to
+// other groups or unused ("holes").  The traversal then finds a child without
+// a popcount and keeps one word per stack entry (hit bits + group word).
+// Root stays at slot 0.  On
 // success the caller owns *out (device, *nslots nodes).  Synchronises s.
 // width 6: every node has at most six children and is re-encoded as the
 // 64-B node of bvh_build.h (kNode6Quads quads per slot); else copied as is

@@ -212,8 +212,8 @@ struct Tracer {
 // Compressed 8-wide BVH traversal (layout: bvh_build.h; after Ylitie et al.
 // 2017).  A "node group" (nhits) holds the unvisited inner children of one
 // node: hit bits 24..31 at position 24 + (slot ^ oct_inv), so the highest bit
-// is the child nearest for this ray's octant, and the node's child base / 8 in
-// bits 0..23 (device layout with holes: child s at base + s).  A "triangle
+// is the child nearest for this ray's octant, and the node's child-group word
+// in bits 0..23 (child s at (word << sc.group_shift) + s, gpu_bvh8_holes).  A "triangle
 // group" (tbase, thits) holds the triangles of the hit leaves.
 // Child slabs are evaluated as t = q * (2^e / d) + (p - o) / d with one fma;
 // each axis is widened by a margin that bounds the fp32 error of that form
@@ -257,8 +257,8 @@ struct Tracer8T {
     float ix, iy, iz, tmin;
     uint32_t oct_rep;  // the ray's inverted octant (0..7) replicated in every byte
     // node group: unvisited hit children in bits 24..31 (bit 24 + (slot ^
-    // octant)), the group's first node / 8 in bits 0..23 (child s of a node
-    // sits at w4 + s, gpu_bvh8_holes) — one word, also one LDS stack entry
+    // octant)), the child-group word in bits 0..23 (child s of a node sits at
+    // (word << group_shift) + s, gpu_bvh8_holes) — one word, also one LDS stack entry
     uint32_t nhits;
     uint32_t tbase, thits;
     uint32_t tbase2, thits2;  // kStep 2: a second triangle group, queued behind (tbase, thits)
