@@ -288,6 +288,33 @@ spt_status spt_bvh_build_stats(const float* tri_verts, uint64_t ntri, const spt_
                                spt_scene_stats* out);
 spt_status spt_scene_destroy(spt_scene scene);
 
+/* Binary scene cache ("a binary scene cache format").  The
+ * reference re-parses its OBJ and rebuilds the OptiX GAS on every run
+ * (main.cpp:288-318 → optix_backend.h:283-364); its pbrt-parser dependency
+ * caches only the parse.  spt_scene_save writes a committed scene to one
+ * file: the BVH in its device layout (node slots, packed child groups), the
+ * slot-ordered triangle / normal / texcoord / orig2slot arrays, albedo,
+ * emission, spheres, material kinds, textures, the scene's spt_config and
+ * spt_scene_stats, and `extra` (extra_bytes opaque application bytes, e.g. the
+ * pbrt camera; may be NULL / 0).  spt_scene_load uploads it onto the current
+ * device with no parse, build or re-layout (stats.build_ms = the load time,
+ * builder as saved); the result renders bit-identically to the saved scene.
+ *
+ * Format (little endian): a fixed header {magic "SPTSCENE", version, the
+ * writer's layout constants (triangle and node quads, node6, group_shift,
+ * sizeof spt_config / spt_scene_stats), counts, section sizes, one 64-bit
+ * checksum per section, spt_config, spt_scene_stats} then the sections in
+ * that order.  Load refuses (SPT_ERR_INVALID) another magic / version /
+ * layout, a size mismatch or a truncated file before touching the device, and
+ * a bad checksum before the scene is returned (its uploads are freed).
+ * spt_scene_cache_info runs all the checks without a device and
+ * reports the saved stats / config / extra size (each out pointer may be
+ * NULL).  spt_scene_load copies at most extra_cap bytes of extra into `extra`
+ * and the full size into *extra_bytes (both may be NULL / 0). */
+spt_status spt_scene_save(spt_scene scene, const char* path, const void* extra, uint64_t extra_bytes);
+spt_status spt_scene_load(const char* path, spt_scene* out, void* extra, uint64_t extra_cap, uint64_t* extra_bytes);
+spt_status spt_scene_cache_info(const char* path, spt_scene_stats* stats, spt_config* cfg, uint64_t* extra_bytes);
+
 /* OptixBackend::intersect (optix_backend.h:422-460) → __raygen__rg
  * (wavefront_isect.cu:80-112): one lane per ray; mask_size == 1 broadcasts
  * mask[0]; masked lanes write nothing; a miss writes tri_id = -1 (t/u/v

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstddef>
@@ -164,6 +165,7 @@ struct spt_scene_t {
     uint32_t nsph = 0;
     uint32_t* mat_kind = nullptr;  // SPT_MAT_* per material (spt_scene_set_material_kinds)
     uint32_t nkind = 0;
+    uint64_t node_bytes = 0;  // bytes behind nodes / nodes8 (spt_scene_save)
     uint32_t stack_depth = 1;
     spt_scene_stats stats{};
     Workspace ws;
@@ -192,6 +194,8 @@ spt_status ensure_device() {
     if (e != hipSuccess || n == 0) return fail(SPT_ERR_NO_DEVICE, "no HIP device visible (%s)", hipGetErrorString(e));
     return SPT_OK;
 }
+
+spt_status upload_textures(spt_scene_t* sc);
 
 template <typename T>
 spt_status upload(T** dst, const void* src, size_t bytes) {
@@ -369,6 +373,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
         }
         sc->nodes8 = (uint4*)holes;
         sc->node6 = width == 6;
+        sc->node_bytes = holes ? (uint64_t)nslots * (width == 6 ? kNode6Quads : kNode8Quads) * 16 : 0;
     }
     auto bail = [&](hipError_t e) {
         (void)hipFree(g.slot2tri);
@@ -402,7 +407,8 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     ss.max_leaf = 3;
     ss.bvh_width = (uint32_t)width;
     ss.builder = SPT_BUILD_GPU_PLOC;
-    ss.device_bytes = (uint64_t)nslots * (width == 6 ? kNode6Quads : kNode8Quads) * 16 + ntri * 3 * 16 * 2 + (with_tc ? ntri * 24 : 0) + ntri * 4;
+    ss.device_bytes = (uint64_t)nslots * (width == 6 ? kNode6Quads : kNode8Quads) * 16 + ntri * (kTriQuads + 3) * 16 +
+                      (with_tc ? ntri * 24 : 0) + ntri * 4;
     ss.build_ms = now_ms() - t0;
     ss.sah_cost = g.sah_cost;
     *out = sc;
@@ -599,11 +605,16 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
                                                  cfg.pack_groups ? &sc->group_shift : nullptr);
             if (he) us = fail(he == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP,
                               "spt_scene_create (BVH8 layout): %s", hipGetErrorString(he));
-            else { sc->nodes8 = (uint4*)holes; sc->node6 = width == 6; }
+            else {
+                sc->nodes8 = (uint4*)holes;
+                sc->node6 = width == 6;
+                sc->node_bytes = holes ? (uint64_t)nslots * (width == 6 ? kNode6Quads : kNode8Quads) * 16 : 0;
+            }
         }
         hfree(compact);
     } else {
         if (!us) us = upload(&sc->nodes, bvh.nodes.data(), bvh.nodes.size() * sizeof(float));
+        if (!us && sc->nodes) sc->node_bytes = bvh.nodes.size() * sizeof(float);
     }
     if (!us) us = upload(&sc->tris, h_tris.data(), h_tris.size() * sizeof(float4));
     if (!us) us = upload(&sc->snrm, h_snrm.data(), h_snrm.size() * sizeof(float4));
@@ -735,7 +746,14 @@ spt_status spt_scene_set_texture(spt_scene sc, uint32_t material, const float* r
         sc->tex_w[material] = width;
         sc->tex_h[material] = height;
     }
-    // rebuild the device arrays: one texel array, one (first, w, h, has) entry per material
+    return upload_textures(sc);
+}
+
+namespace {
+
+// Rebuild the texture device arrays from the host copies (caller holds sc->mu):
+// one texel array, one (first, w, h, has) entry per material.
+spt_status upload_textures(spt_scene_t* sc) {
     std::vector<uint4> info(sc->tex_img.size());
     std::vector<float4> all;
     uint32_t used = 0;
@@ -756,6 +774,8 @@ spt_status spt_scene_set_texture(spt_scene sc, uint32_t material, const float* r
     }
     return SPT_OK;
 }
+
+}  // namespace
 
 spt_status spt_scene_set_spheres(spt_scene sc, const float* center_radius, const int32_t* mat_id, uint32_t n) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: NULL scene");
@@ -838,6 +858,374 @@ spt_status spt_scene_destroy(spt_scene sc) {
     if (!sc) return SPT_OK;
     sc->release();
     delete sc;
+    return SPT_OK;
+}
+
+// ---------------------------------------------------------------- scene cache
+// spt_scene_save / spt_scene_load / spt_scene_cache_info (include/spt.h).
+namespace {
+
+constexpr char kCacheMagic[8] = {'S', 'P', 'T', 'S', 'C', 'E', 'N', 'E'};
+constexpr uint32_t kCacheVersion = 1;
+constexpr size_t kCacheChunk = size_t(64) << 20;  // host staging per read / write / download
+
+// Sections, in file order.
+enum : uint32_t {
+    kSecNodes, kSecTris, kSecSnrm, kSecTc, kSecOrig2Slot, kSecAlbedo, kSecEmission, kSecSpheres, kSecSphMat,
+    kSecKinds, kSecTexDims, kSecTexels, kSecExtra, kNumSecs
+};
+const char* const kSecName[kNumSecs] = {"nodes", "triangles", "normals", "texcoords", "orig2slot", "albedo",
+                                        "emission", "spheres", "sphere materials", "material kinds",
+                                        "texture sizes", "texels", "extra"};
+
+struct CacheHeader {
+    char magic[8];
+    uint32_t version, header_bytes;
+    uint32_t tri_quads, node_quads;      // the writer's layout: 16-B quads per triangle slot / node slot
+    uint32_t node6, group_shift;
+    uint32_t config_bytes, stats_bytes;  // sizeof(spt_config), sizeof(spt_scene_stats)
+    uint32_t stack_depth, nmat, nemit, nsph, nkind, ntexmat;
+    uint64_t ntri;
+    uint64_t bytes[kNumSecs];
+    uint64_t sum[kNumSecs];
+    spt_config cfg;
+    spt_scene_stats stats;
+};
+
+// 16-B quads per node slot of a scene of this build with the given width.
+uint32_t node_quads_of(uint32_t width, uint32_t node6) {
+    return width == 2 ? 4u : (node6 ? (uint32_t)kNode6Quads : (uint32_t)kNode8Quads);
+}
+
+// Section checksum: four 64-bit multiply-xorshift lanes over 32-B blocks
+// (streamed in any split), folded with the length.
+class CacheHash {
+    static constexpr uint64_t kMul = 0x9fb21c651e98df25ull;
+    uint64_t h_[4] = {0x243f6a8885a308d3ull, 0x13198a2e03707344ull, 0xa4093822299f31d0ull, 0x082efa98ec4e6c89ull};
+    uint8_t tail_[32];
+    size_t nt_ = 0;
+    uint64_t len_ = 0;
+    void block(const uint8_t* p) {
+        for (int k = 0; k < 4; k++) {
+            uint64_t w;
+            std::memcpy(&w, p + 8 * k, 8);
+            h_[k] = (h_[k] ^ w) * kMul;
+            h_[k] ^= h_[k] >> 31;
+        }
+    }
+
+  public:
+    void update(const void* data, size_t n) {
+        const uint8_t* p = (const uint8_t*)data;
+        len_ += n;
+        if (nt_) {
+            const size_t take = std::min(32 - nt_, n);
+            std::memcpy(tail_ + nt_, p, take);
+            nt_ += take; p += take; n -= take;
+            if (nt_ < 32) return;
+            block(tail_);
+            nt_ = 0;
+        }
+        for (; n >= 32; p += 32, n -= 32) block(p);
+        std::memcpy(tail_, p, n);
+        nt_ = n;
+    }
+    uint64_t digest() {
+        std::memset(tail_ + nt_, 0, 32 - nt_);
+        block(tail_);
+        uint64_t r = len_;
+        for (int k = 0; k < 4; k++) {
+            r = (r ^ h_[k]) * kMul;
+            r ^= r >> 29;
+        }
+        return r;
+    }
+};
+
+struct FileCloser {
+    FILE* f;
+    ~FileCloser() { if (f) std::fclose(f); }
+};
+
+// The header checks of spt_scene_load / spt_scene_cache_info (no device).
+spt_status cache_read_header(FILE* f, const char* path, const char* what, CacheHeader& h) {
+    if (std::fseek(f, 0, SEEK_END) != 0) return fail(SPT_ERR_IO, "%s: cannot seek %s", what, path);
+    const long long fsize = (long long)std::ftell(f);
+    std::rewind(f);
+    std::memset(&h, 0, sizeof(h));
+    if (fsize < (long long)sizeof(h) || std::fread(&h, sizeof(h), 1, f) != 1)
+        return fail(SPT_ERR_INVALID, "%s: %s is not a scene cache (shorter than its header)", what, path);
+    if (std::memcmp(h.magic, kCacheMagic, 8) != 0)
+        return fail(SPT_ERR_INVALID, "%s: %s is not a scene cache (bad magic)", what, path);
+    if (h.version != kCacheVersion || h.header_bytes != sizeof(CacheHeader) || h.config_bytes != sizeof(spt_config) ||
+        h.stats_bytes != sizeof(spt_scene_stats))
+        return fail(SPT_ERR_INVALID, "%s: %s has version %u / header %u B (this library reads version %u / %zu B)",
+                    what, path, h.version, h.header_bytes, kCacheVersion, sizeof(CacheHeader));
+    const uint32_t width = h.stats.bvh_width;
+    if ((width != 2 && width != 6 && width != 8) || h.node6 != (width == 6 ? 1u : 0u))
+        return fail(SPT_ERR_INVALID, "%s: %s: BVH width %u / node6 %u", what, path, width, h.node6);
+    if (h.tri_quads != (uint32_t)kTriQuads || h.node_quads != node_quads_of(width, h.node6) ||
+        (h.group_shift != 0 && h.group_shift != 3))
+        return fail(SPT_ERR_INVALID, "%s: %s was written with another layout (triangle %u / node %u quads, group "
+                    "shift %u; this library: %u / %u)", what, path, h.tri_quads, h.node_quads, h.group_shift,
+                    (uint32_t)kTriQuads, node_quads_of(width, h.node6));
+    if (h.ntri >= kMaxTriangles || h.ntri != h.stats.ntri || h.nmat == 0 || h.nsph > 256 || h.stack_depth == 0)
+        return fail(SPT_ERR_INVALID, "%s: %s: bad counts (ntri %llu, nmat %u, spheres %u, stack %u)", what, path,
+                    (unsigned long long)h.ntri, h.nmat, h.nsph, h.stack_depth);
+    const uint64_t n = h.ntri;
+    const uint64_t want[kNumSecs] = {
+        h.bytes[kSecNodes], n * kTriQuads * 16, n * 48, h.bytes[kSecTc] ? n * 24 : 0, n * 4, (uint64_t)h.nmat * 12,
+        (uint64_t)h.nemit * 12, (uint64_t)h.nsph * 16, (uint64_t)h.nsph * 4, (uint64_t)h.nkind * 4,
+        (uint64_t)h.ntexmat * 8, h.bytes[kSecTexels], h.bytes[kSecExtra]};
+    for (uint32_t s = 0; s < kNumSecs; s++)
+        if (h.bytes[s] != want[s])
+            return fail(SPT_ERR_INVALID, "%s: %s: section %s holds %llu bytes, expected %llu", what, path, kSecName[s],
+                        (unsigned long long)h.bytes[s], (unsigned long long)want[s]);
+    if (h.bytes[kSecNodes] % ((uint64_t)h.node_quads * 16) != 0 || (n > 0 && h.bytes[kSecNodes] == 0) ||
+        h.bytes[kSecTexels] % 16 != 0)
+        return fail(SPT_ERR_INVALID, "%s: %s: node / texel sections are not whole records", what, path);
+    long long total = (long long)sizeof(CacheHeader);
+    for (uint32_t s = 0; s < kNumSecs; s++) total += (long long)h.bytes[s];
+    if (total != fsize)
+        return fail(SPT_ERR_INVALID, "%s: %s holds %lld bytes, its header describes %lld (truncated?)", what, path,
+                    fsize, total);
+    return SPT_OK;
+}
+
+// Read section s (h.bytes[s] bytes at the file position) into dst, checking its sum.
+spt_status cache_read_section(FILE* f, const char* path, const char* what, const CacheHeader& h, uint32_t s,
+                              std::vector<uint8_t>& dst) {
+    dst.resize(h.bytes[s]);
+    CacheHash hash;
+    for (size_t off = 0; off < dst.size(); off += kCacheChunk) {
+        const size_t len = std::min(kCacheChunk, dst.size() - off);
+        if (std::fread(dst.data() + off, 1, len, f) != len)
+            return fail(SPT_ERR_IO, "%s: short read of section %s of %s", what, kSecName[s], path);
+        hash.update(dst.data() + off, len);
+    }
+    if (hash.digest() != h.sum[s])
+        return fail(SPT_ERR_INVALID, "%s: %s: checksum mismatch in section %s", what, path, kSecName[s]);
+    return SPT_OK;
+}
+
+// Texture section checks: one (w, h) pair per material, texels = their sum.
+spt_status cache_check_textures(const char* path, const char* what, const CacheHeader& h, const uint32_t* dims) {
+    uint64_t texels = 0;
+    for (uint32_t m = 0; m < h.ntexmat; m++) {
+        const uint64_t wh = (uint64_t)dims[2 * m] * dims[2 * m + 1];
+        if (wh > (1ull << 26)) return fail(SPT_ERR_INVALID, "%s: %s: texture %u is %llu texels", what, path, m,
+                                           (unsigned long long)wh);
+        texels += wh;
+    }
+    if (texels * 16 != h.bytes[kSecTexels])
+        return fail(SPT_ERR_INVALID, "%s: %s: texture sizes describe %llu texels, the section holds %llu", what, path,
+                    (unsigned long long)texels, (unsigned long long)(h.bytes[kSecTexels] / 16));
+    return SPT_OK;
+}
+
+}  // namespace
+
+spt_status spt_scene_save(spt_scene sc, const char* path, const void* extra, uint64_t extra_bytes) {
+    static const char* what = "spt_scene_save";
+    if (!sc || !path) return fail(SPT_ERR_INVALID, "%s: NULL argument", what);
+    if (extra_bytes && !extra) return fail(SPT_ERR_INVALID, "%s: extra is NULL with %llu bytes", what,
+                                           (unsigned long long)extra_bytes);
+    std::lock_guard<std::mutex> lk(sc->mu);
+    CacheHeader h;
+    std::memset(&h, 0, sizeof(h));
+    std::memcpy(h.magic, kCacheMagic, 8);
+    h.version = kCacheVersion;
+    h.header_bytes = sizeof(CacheHeader);
+    h.tri_quads = kTriQuads;
+    h.node_quads = node_quads_of(sc->stats.bvh_width, sc->node6);
+    h.node6 = sc->node6;
+    h.group_shift = sc->group_shift;
+    h.config_bytes = sizeof(spt_config);
+    h.stats_bytes = sizeof(spt_scene_stats);
+    h.stack_depth = sc->stack_depth;
+    h.nmat = sc->nmat;
+    h.nemit = sc->nemit;
+    h.nsph = sc->nsph;
+    h.nkind = sc->nkind;
+    h.ntexmat = sc->ntex;
+    h.ntri = sc->ntri;
+    h.cfg = sc->cfg;
+    h.stats = sc->stats;
+    // textures: their host copies
+    std::vector<uint32_t> dims(2 * (size_t)sc->ntex);
+    std::vector<float4> texels;
+    for (uint32_t m = 0; m < sc->ntex; m++) {
+        dims[2 * m] = sc->tex_w[m];
+        dims[2 * m + 1] = sc->tex_h[m];
+        texels.insert(texels.end(), sc->tex_img[m].begin(), sc->tex_img[m].end());
+    }
+    struct Src { const void* dev; const void* host; uint64_t bytes; };
+    const uint64_t n = sc->ntri;
+    const Src src[kNumSecs] = {
+        {sc->nodes8 ? (const void*)sc->nodes8 : (const void*)sc->nodes, nullptr, sc->node_bytes},
+        {sc->tris, nullptr, n * kTriQuads * 16},
+        {sc->snrm, nullptr, n * 48},
+        {sc->tc, nullptr, sc->tc ? n * 24 : 0},
+        {sc->orig2slot, nullptr, n * 4},
+        {sc->albedo, nullptr, (uint64_t)sc->nmat * 12},
+        {sc->emission, nullptr, (uint64_t)sc->nemit * 12},
+        {sc->spheres, nullptr, (uint64_t)sc->nsph * 16},
+        {sc->sph_mat, nullptr, (uint64_t)sc->nsph * 4},
+        {sc->mat_kind, nullptr, (uint64_t)sc->nkind * 4},
+        {nullptr, dims.data(), dims.size() * 4},
+        {nullptr, texels.data(), texels.size() * 16},
+        {nullptr, extra, extra_bytes}};
+    for (uint32_t s = 0; s < kNumSecs; s++)
+        if (src[s].bytes && !src[s].dev && !src[s].host)
+            return fail(SPT_ERR_INVALID, "%s: the scene has no %s array", what, kSecName[s]);
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(SPT_ERR_IO, "%s: cannot open %s: %s", what, path, std::strerror(errno));
+    FileCloser closer{f};
+    if (std::fwrite(&h, sizeof(h), 1, f) != 1) return fail(SPT_ERR_IO, "%s: short write to %s", what, path);
+    std::vector<uint8_t> stage;
+    for (uint32_t s = 0; s < kNumSecs; s++) {
+        CacheHash hash;
+        for (uint64_t off = 0; off < src[s].bytes; off += kCacheChunk) {
+            const size_t len = (size_t)std::min<uint64_t>(kCacheChunk, src[s].bytes - off);
+            const uint8_t* p;
+            if (src[s].dev) {
+                stage.resize(len);
+                HIP_TRY(hipMemcpy(stage.data(), (const uint8_t*)src[s].dev + off, len, hipMemcpyDeviceToHost));
+                p = stage.data();
+            } else {
+                p = (const uint8_t*)src[s].host + off;
+            }
+            hash.update(p, len);
+            if (std::fwrite(p, 1, len, f) != len) return fail(SPT_ERR_IO, "%s: short write to %s", what, path);
+        }
+        h.bytes[s] = src[s].bytes;
+        h.sum[s] = hash.digest();
+    }
+    std::rewind(f);
+    if (std::fwrite(&h, sizeof(h), 1, f) != 1) return fail(SPT_ERR_IO, "%s: short write to %s", what, path);
+    closer.f = nullptr;
+    return std::fclose(f) == 0 ? SPT_OK : fail(SPT_ERR_IO, "%s: closing %s failed", what, path);
+}
+
+spt_status spt_scene_cache_info(const char* path, spt_scene_stats* stats, spt_config* cfg, uint64_t* extra_bytes) {
+    static const char* what = "spt_scene_cache_info";
+    if (!path) return fail(SPT_ERR_INVALID, "%s: NULL path", what);
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(SPT_ERR_IO, "%s: cannot open %s: %s", what, path, std::strerror(errno));
+    FileCloser closer{f};
+    CacheHeader h;
+    spt_status st = cache_read_header(f, path, what, h);
+    if (st) return st;
+    std::vector<uint8_t> buf;
+    for (uint32_t s = 0; s < kNumSecs; s++) {
+        if (s == kSecTexDims) {  // small (8 B per material): read whole and check against the texel section
+            if ((st = cache_read_section(f, path, what, h, s, buf))) return st;
+            if ((st = cache_check_textures(path, what, h, (const uint32_t*)buf.data()))) return st;
+            continue;
+        }
+        // sums only: stream through one chunk at a time
+        CacheHash hash;
+        for (uint64_t off = 0; off < h.bytes[s]; off += kCacheChunk) {
+            const size_t len = (size_t)std::min<uint64_t>(kCacheChunk, h.bytes[s] - off);
+            buf.resize(len);
+            if (std::fread(buf.data(), 1, len, f) != len)
+                return fail(SPT_ERR_IO, "%s: short read of section %s of %s", what, kSecName[s], path);
+            hash.update(buf.data(), len);
+        }
+        if (hash.digest() != h.sum[s])
+            return fail(SPT_ERR_INVALID, "%s: %s: checksum mismatch in section %s", what, path, kSecName[s]);
+    }
+    if (stats) *stats = h.stats;
+    if (cfg) *cfg = h.cfg;
+    if (extra_bytes) *extra_bytes = h.bytes[kSecExtra];
+    return SPT_OK;
+}
+
+spt_status spt_scene_load(const char* path, spt_scene* out, void* extra, uint64_t extra_cap, uint64_t* extra_bytes) {
+    static const char* what = "spt_scene_load";
+    if (!path || !out) return fail(SPT_ERR_INVALID, "%s: NULL argument", what);
+    *out = nullptr;
+    if (extra_cap && !extra) return fail(SPT_ERR_INVALID, "%s: extra is NULL with capacity %llu", what,
+                                         (unsigned long long)extra_cap);
+    const double t0 = now_ms();
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(SPT_ERR_IO, "%s: cannot open %s: %s", what, path, std::strerror(errno));
+    FileCloser closer{f};
+    CacheHeader h;
+    spt_status st = cache_read_header(f, path, what, h);
+    if (!st) st = check_config(h.cfg);
+    if (st) return st;
+    if ((st = ensure_device())) return st;
+    spt_scene_t* sc = new spt_scene_t();
+    auto bail = [&](spt_status e) {
+        sc->release();
+        delete sc;
+        return e;
+    };
+    sc->cfg = h.cfg;
+    (void)hipGetDevice(&sc->device);
+    sc->ntri = h.ntri;
+    sc->node6 = h.node6;
+    sc->group_shift = h.group_shift;
+    sc->stack_depth = h.stack_depth;
+    std::vector<uint8_t> buf;
+    for (uint32_t s = 0; s < kNumSecs; s++) {
+        if ((st = cache_read_section(f, path, what, h, s, buf))) return bail(st);
+        switch (s) {
+            case kSecNodes:
+                st = h.stats.bvh_width == 2 ? upload(&sc->nodes, buf.data(), buf.size())
+                                            : upload(&sc->nodes8, buf.data(), buf.size());
+                sc->node_bytes = buf.size();
+                break;
+            case kSecTris: st = upload(&sc->tris, buf.data(), buf.size()); break;
+            case kSecSnrm: st = upload(&sc->snrm, buf.data(), buf.size()); break;
+            case kSecTc: st = upload(&sc->tc, buf.data(), buf.size()); break;
+            case kSecOrig2Slot: st = upload(&sc->orig2slot, buf.data(), buf.size()); break;
+            case kSecAlbedo: {
+                st = upload(&sc->albedo, buf.data(), buf.size());
+                const float* a = (const float*)buf.data();
+                bool unit = true;
+                for (size_t i = 0; i < buf.size() / 4; i++) unit = unit && a[i] == 1.0f;
+                sc->albedo_unit = unit;
+                sc->nmat = h.nmat;
+                break;
+            }
+            case kSecEmission: st = upload(&sc->emission, buf.data(), buf.size()); sc->nemit = h.nemit; break;
+            case kSecSpheres: st = upload(&sc->spheres, buf.data(), buf.size()); break;
+            case kSecSphMat: st = upload(&sc->sph_mat, buf.data(), buf.size()); sc->nsph = h.nsph; break;
+            case kSecKinds: st = upload(&sc->mat_kind, buf.data(), buf.size()); sc->nkind = h.nkind; break;
+            case kSecTexDims: {
+                const uint32_t* dims = (const uint32_t*)buf.data();
+                if ((st = cache_check_textures(path, what, h, dims))) break;
+                sc->tex_img.resize(h.ntexmat);
+                sc->tex_w.resize(h.ntexmat);
+                sc->tex_h.resize(h.ntexmat);
+                for (uint32_t m = 0; m < h.ntexmat; m++) {
+                    sc->tex_w[m] = dims[2 * m];
+                    sc->tex_h[m] = dims[2 * m + 1];
+                }
+                break;
+            }
+            case kSecTexels: {
+                const float4* t = (const float4*)buf.data();
+                for (uint32_t m = 0; m < h.ntexmat; m++) {
+                    const size_t wh = (size_t)sc->tex_w[m] * sc->tex_h[m];
+                    sc->tex_img[m].assign(t, t + wh);
+                    t += wh;
+                }
+                st = upload_textures(sc);
+                break;
+            }
+            case kSecExtra:
+                if (extra && extra_cap) std::memcpy(extra, buf.data(), (size_t)std::min<uint64_t>(extra_cap, buf.size()));
+                if (extra_bytes) *extra_bytes = buf.size();
+                break;
+        }
+        if (st) return bail(st);
+    }
+    sc->stats = h.stats;
+    sc->stats.build_ms = now_ms() - t0;
+    *out = sc;
     return SPT_OK;
 }
 

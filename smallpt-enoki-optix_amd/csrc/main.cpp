@@ -2,10 +2,11 @@
 // load an OBJ (or a pbrt-v3 scene), commit the scene, render, normalise, read
 // back, write a PFM, print the wall time.  Every constant defaults to the
 // reference's; a .pbrt file's camera, film size and infinite light replace
-// them, and flags override both.
+// them, and flags override both.  A .sptc file is a binary scene cache
+// (spt_scene_load: no parse, no BVH build); --save-cache writes one after commit.
 //
-//   spt_render_cli [scene.obj|scene.pbrt] [-w W] [-h H] [-s spp] [-d casts] [-o out.pfm]
-//                  [--wavefront paths] [--rr depth] [--rng-x-first] [--device N]
+//   spt_render_cli [scene.obj|scene.pbrt|scene.sptc] [-w W] [-h H] [-s spp] [-d casts] [-o out.pfm]
+//                  [--wavefront paths] [--rr depth] [--rng-x-first] [--device N] [--save-cache f.sptc]
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -20,6 +21,7 @@
 int main(int argc, char** argv) {
     std::string obj = "mitsuba.obj";  // main.cpp:365
     std::string out = "wurst.pfm";    // main.cpp:442
+    std::string cache_out;
     int device = 0;
     spt_render_params p;
     spt_default_params(&p);            // 512 x 512, 100 spp, 2 casts (main.cpp:357-361)
@@ -39,13 +41,23 @@ int main(int argc, char** argv) {
         else if (a == "--rr") p.rr_start_depth = (uint32_t)std::atoi(next());
         else if (a == "--rng-x-first") p.rng_order = SPT_RNG_X_FIRST;
         else if (a == "--device") device = std::atoi(next());
+        else if (a == "--save-cache") cache_out = next();
         else if (!a.empty() && a[0] != '-') obj = a;
         else { std::cerr << "unknown flag " << a << "\n"; return 2; }
     }
     try {
         spt::Scene scene;
-        scene.add_triangle_mesh(obj);  // main.cpp:365
-        scene.commit(device);          // main.cpp:366
+        auto tl = std::chrono::steady_clock::now();
+        if (spt::ends_with(obj, ".sptc")) {
+            scene.load(obj, device);
+        } else {
+            scene.add_triangle_mesh(obj);  // main.cpp:365
+            scene.commit(device);          // main.cpp:366
+        }
+        std::cerr << "scene ready in "
+                  << std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tl).count() << " ms"
+                  << std::endl;
+        if (!cache_out.empty()) scene.save(cache_out);
         const spt_pbrt_info& pi = scene.pbrt_info();
         if (pi.has_camera) {
             p.camera = pi.camera;

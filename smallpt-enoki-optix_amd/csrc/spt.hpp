@@ -43,8 +43,11 @@ class Scene {
     Scene(const Scene&) = delete;
     Scene& operator=(const Scene&) = delete;
 
-    void add_triangle_mesh(const std::string& path) { mesh_.reset(new Mesh(path)); }  // main.cpp:288
-    void commit(int device = 0) {                                                            // main.cpp:312
+    void add_triangle_mesh(const std::string& path) {  // main.cpp:288
+        mesh_.reset(new Mesh(path));
+        pbrt_ = mesh_->pbrt;
+    }
+    void commit(int device = 0) {                      // main.cpp:312
         if (!mesh_) throw std::runtime_error("Scene::commit: no mesh added");
         check(spt_init(device), "spt_init");
         const spt_mesh& m = mesh_->m;
@@ -52,15 +55,33 @@ class Scene {
                                m.mat_id, &scene_),
               "spt_scene_create");
     }
+    // Binary scene cache (spt_scene_save / spt_scene_load): the committed
+    // scene, with the pbrt camera / film / sky as its extra bytes.
+    void save(const std::string& path) const {
+        const bool has = pbrt_.has_camera || pbrt_.has_env;
+        check(spt_scene_save(scene_, path.c_str(), has ? &pbrt_ : nullptr, has ? sizeof(pbrt_) : 0), "spt_scene_save");
+    }
+    void load(const std::string& path, int device = 0) {
+        check(spt_init(device), "spt_init");
+        if (scene_) spt_scene_destroy(scene_);
+        scene_ = nullptr;
+        mesh_.reset();
+        pbrt_ = spt_pbrt_info{};
+        uint64_t n = 0;
+        check(spt_scene_load(path.c_str(), &scene_, &pbrt_, sizeof(pbrt_), &n), "spt_scene_load");
+        if (n != 0 && n != sizeof(pbrt_)) throw std::runtime_error(path + ": extra bytes are not an spt_pbrt_info");
+        if (n == 0) pbrt_ = spt_pbrt_info{};
+    }
     void render(const spt_render_params& p, float* film_dev, spt_render_stats* stats, void* stream = nullptr) {
         check(spt_render(scene_, &p, film_dev, stats, stream), "spt_render");
     }
     spt_scene handle() const { return scene_; }
-    const spt_mesh& mesh() const { return mesh_->m; }
-    const spt_pbrt_info& pbrt_info() const { return mesh_->pbrt; }
+    const spt_mesh& mesh() const { return mesh_->m; }  // not after load()
+    const spt_pbrt_info& pbrt_info() const { return pbrt_; }
 
   private:
     std::unique_ptr<Mesh> mesh_;
+    spt_pbrt_info pbrt_{};
     spt_scene scene_ = nullptr;
 };
 

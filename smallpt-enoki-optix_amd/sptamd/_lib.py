@@ -15,6 +15,7 @@ REPO_ROOT = os.path.dirname(PKG_ROOT)
 LIB_PATH = os.environ.get("SPT_LIB") or os.path.join(PKG_ROOT, "build", "libspt.so")
 
 SPT_OK = 0
+SPT_ERR_INVALID, SPT_ERR_HIP, SPT_ERR_NO_DEVICE, SPT_ERR_OOM, SPT_ERR_IO, SPT_ERR_LIMIT = 1, 2, 3, 4, 5, 6
 SPT_RNG_Y_FIRST = 0
 SPT_RNG_X_FIRST = 1
 SPT_FLAG_TIMING = 1
@@ -33,6 +34,7 @@ EXPORTED = [
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write", "spt_pbrt_load",
     "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
     "spt_bvh_build_stats", "spt_scene_set_texture", "spt_scene_set_spheres", "spt_scene_set_material_kinds",
+    "spt_scene_save", "spt_scene_load", "spt_scene_cache_info",
 ]
 SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
@@ -166,6 +168,9 @@ def _load() -> ctypes.CDLL:
         "spt_scene_set_texture": (i32, [vp, u32, vp, u32, u32]),
         "spt_scene_set_spheres": (i32, [vp, vp, vp, u32]),
         "spt_scene_set_material_kinds": (i32, [vp, vp, u32]),
+        "spt_scene_save": (i32, [vp, c_char_p, vp, u64]),
+        "spt_scene_load": (i32, [c_char_p, POINTER(vp), vp, u64, POINTER(u64)]),
+        "spt_scene_cache_info": (i32, [c_char_p, POINTER(SceneStats), POINTER(Config), POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

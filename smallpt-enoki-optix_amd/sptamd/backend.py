@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -171,6 +172,34 @@ class HipBackend:
         check(lib.spt_scene_set_texture(self._scene, material, img.ctypes.data, img.shape[1], img.shape[0]),
               "spt_scene_set_texture")
 
+    def save(self, path: str, extra: bytes = b"") -> None:
+        """spt_scene_save: the committed scene (BVH, arrays, materials) + extra bytes to one file."""
+        check(lib.spt_scene_save(self._scene, os.fsencode(path), extra or None, len(extra)), "spt_scene_save")
+
+    def load(self, path: str, device: int = 0) -> bytes:
+        """spt_scene_load onto `device`: no parse, no build.  Returns the file's extra bytes."""
+        self.init(device)
+        if self._scene.value:
+            lib.spt_scene_destroy(self._scene)
+            self._scene = ctypes.c_void_p()
+        n, cap = ctypes.c_uint64(), 1 << 16
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            check(lib.spt_scene_load(os.fsencode(path), ctypes.byref(self._scene), buf, cap, ctypes.byref(n)),
+                  "spt_scene_load")
+            if n.value <= cap:
+                break
+            lib.spt_scene_destroy(self._scene)      # a larger extra than the first buffer: once more
+            self._scene = ctypes.c_void_p()
+            cap = n.value
+        cfg = Config()
+        check(lib.spt_scene_get_config(self._scene, ctypes.byref(cfg)), "spt_scene_get_config")
+        self._applied = bytes(cfg)
+        st = SceneStats()
+        check(lib.spt_scene_get_stats(self._scene, ctypes.byref(st)), "spt_scene_get_stats")
+        self.stats = st.as_dict()
+        return buf.raw[:n.value]
+
     @property
     def handle(self):
         return self._scene
@@ -319,6 +348,24 @@ class Scene:
         if m.get("kinds") is not None:
             self.backend.set_material_kinds(m["kinds"])
 
+    def save(self, path: str) -> None:
+        """Binary scene cache of the committed scene (spt_scene_save); pbrt_info rides
+        along as the extra bytes (an spt_pbrt_info, as spt_render_cli --save-cache writes)."""
+        from .scenes import pbrt_info_to_c
+        self.backend.save(path, bytes(pbrt_info_to_c(self.pbrt_info)) if self.pbrt_info is not None else b"")
+
+    @classmethod
+    def load(cls, path: str, device: int = 0, config: Optional[Config] = None) -> "Scene":
+        """A committed Scene from a spt_scene_save file (no parse, no BVH build); mesh stays None."""
+        sc = cls(config)
+        extra = sc.backend.load(path, device)
+        if len(extra) == ctypes.sizeof(_lib.PbrtInfo):
+            from .scenes import pbrt_info_from_c
+            sc.pbrt_info = pbrt_info_from_c(_lib.PbrtInfo.from_buffer_copy(extra))
+        elif extra:
+            raise ValueError(f"{path}: {len(extra)} extra bytes are not an spt_pbrt_info")
+        return sc
+
     def intersect(self, ray: Ray3, active=None):           # main.cpp:320-340
         return self.backend.intersect(ray, active)
 
@@ -335,6 +382,15 @@ class Scene:
         check(lib.spt_render(self.backend.handle, ctypes.byref(params), film.data_ptr(), ctypes.byref(st),
                              _stream_handle(stream)), "spt_render")
         return film, st.as_dict()
+
+
+def scene_cache_info(path: str) -> dict:
+    """spt_scene_cache_info: checks a scene cache file (header, sizes, every
+    section's checksum) without a device; returns its stats, config and extra size."""
+    st, cfg, n = SceneStats(), Config(), ctypes.c_uint64()
+    check(lib.spt_scene_cache_info(os.fsencode(path), ctypes.byref(st), ctypes.byref(cfg), ctypes.byref(n)),
+          "spt_scene_cache_info")
+    return {"stats": st.as_dict(), "config": cfg.as_dict(), "extra_bytes": n.value}
 
 
 def write_pfm(path: str, film: np.ndarray) -> None:

@@ -413,12 +413,37 @@ def load_pbrt(path: str):
         mesh = _mesh_from_c(m)
     finally:
         _lib.lib.spt_mesh_free(ctypes.byref(m))
+    return mesh, pbrt_info_from_c(info)
+
+
+def pbrt_info_from_c(info: "_lib.PbrtInfo") -> dict:
+    """spt_pbrt_info -> load_pbrt's info dict."""
     c = info.camera
     cam = dict(look_from=tuple(c.look_from), look_at=tuple(c.look_at), up=tuple(c.up), lens_radius=c.lens_radius,
                focal_dist=c.focal_dist, fov_y=c.fov_y, film_size_y=c.film_size_y) if info.has_camera else None
-    return mesh, dict(camera=cam, fov_deg=info.fov_deg, xres=info.xres, yres=info.yres,
-                      env=tuple(info.env) if info.has_env else None, shapes=info.shapes,
-                      shapes_skipped=info.shapes_skipped, instances=info.instances)
+    return dict(camera=cam, fov_deg=info.fov_deg, xres=info.xres, yres=info.yres,
+                env=tuple(info.env) if info.has_env else None, shapes=info.shapes,
+                shapes_skipped=info.shapes_skipped, instances=info.instances)
+
+
+def pbrt_info_to_c(d: dict) -> "_lib.PbrtInfo":
+    """load_pbrt's info dict -> spt_pbrt_info (the scene cache's extra bytes,
+    shared with spt_render_cli --save-cache)."""
+    info = _lib.PbrtInfo()
+    cam = d.get("camera")
+    if cam is not None:
+        info.has_camera = 1
+        for k in ("look_from", "look_at", "up"):
+            getattr(info.camera, k)[:] = [float(x) for x in cam[k]]
+        for k in ("lens_radius", "focal_dist", "fov_y", "film_size_y"):
+            setattr(info.camera, k, cam[k])
+    info.fov_deg, info.xres, info.yres = d.get("fov_deg", 90.0), d.get("xres", 640), d.get("yres", 480)
+    if d.get("env") is not None:
+        info.has_env = 1
+        info.env[:] = [float(x) for x in d["env"]]
+    info.shapes, info.shapes_skipped, info.instances = d.get("shapes", 0), d.get("shapes_skipped", 0), \
+        d.get("instances", 0)
+    return info
 
 
 def _write_ply(path: str, pos: np.ndarray, nrm: Optional[np.ndarray], tris: np.ndarray, binary: bool = True) -> None:
