@@ -942,9 +942,16 @@ class CacheHash {
     }
 };
 
+// Closes f when still set; a file being written (unlink_path) is then also
+// removed, so a failed spt_scene_save leaves no partial cache behind.
 struct FileCloser {
     FILE* f;
-    ~FileCloser() { if (f) std::fclose(f); }
+    const char* unlink_path = nullptr;
+    ~FileCloser() {
+        if (!f) return;
+        std::fclose(f);
+        if (unlink_path) std::remove(unlink_path);
+    }
 };
 
 // The header checks of spt_scene_load / spt_scene_cache_info (no device).
@@ -1080,7 +1087,7 @@ spt_status spt_scene_save(spt_scene sc, const char* path, const void* extra, uin
             return fail(SPT_ERR_INVALID, "%s: the scene has no %s array", what, kSecName[s]);
     FILE* f = std::fopen(path, "wb");
     if (!f) return fail(SPT_ERR_IO, "%s: cannot open %s: %s", what, path, std::strerror(errno));
-    FileCloser closer{f};
+    FileCloser closer{f, path};
     if (std::fwrite(&h, sizeof(h), 1, f) != 1) return fail(SPT_ERR_IO, "%s: short write to %s", what, path);
     std::vector<uint8_t> stage;
     for (uint32_t s = 0; s < kNumSecs; s++) {
@@ -1104,7 +1111,9 @@ spt_status spt_scene_save(spt_scene sc, const char* path, const void* extra, uin
     std::rewind(f);
     if (std::fwrite(&h, sizeof(h), 1, f) != 1) return fail(SPT_ERR_IO, "%s: short write to %s", what, path);
     closer.f = nullptr;
-    return std::fclose(f) == 0 ? SPT_OK : fail(SPT_ERR_IO, "%s: closing %s failed", what, path);
+    if (std::fclose(f) == 0) return SPT_OK;
+    std::remove(path);
+    return fail(SPT_ERR_IO, "%s: closing %s failed", what, path);
 }
 
 spt_status spt_scene_cache_info(const char* path, spt_scene_stats* stats, spt_config* cfg, uint64_t* extra_bytes) {

@@ -150,6 +150,9 @@ def test_cache_damage_refused(tmp_path):
     assert e.value.code == _lib.SPT_ERR_IO
     t = sptamd.Scene.load(path)                # the good file still loads
     assert t.backend.stats["ntri"] == s.backend.stats["ntri"]
+    with pytest.raises(sptamd.SptError) as e:   # an unwritable path
+        s.save(str(tmp_path / "no" / "such" / "dir.sptc"))
+    assert e.value.code == _lib.SPT_ERR_IO
 
 
 def test_cli_cache_roundtrip(tmp_path):
