@@ -357,7 +357,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
-            "pipeline_rule": "auto: fused for tiles of <= 16M paths, else wavefront (DESIGN.md §6)"
+            "pipeline_rule": "auto: fused for tiles of <= 32M paths, else wavefront (DESIGN.md §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
                        "workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"

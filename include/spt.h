@@ -81,7 +81,7 @@ enum {
     SPT_FLAG_FUSED = 4u,           /* one persistent trace+shade kernel per sample chunk */
     SPT_FLAG_WAVEFRONT = 8u,       /* isect / shade / refill kernels over path queues
                                       (neither flag: spt_config.pipeline; AUTO = fused iff
-                                      the tile has at most fused_max_paths = 16M paths, or
+                                      the tile has at most fused_max_paths = 32M paths, or
                                       at most wavefront_paths when that is set) */
     SPT_FLAG_TIMING_ALL = 16u      /* with SPT_FLAG_TIMING: also shade / refill / resolve launches */
 };
@@ -201,7 +201,7 @@ typedef struct spt_config {
     uint32_t stack_slack;           /* extra LDS stack entries per lane (0)                  [0..64] */
     /* --- spt_render */
     uint32_t pipeline;              /* SPT_PIPELINE_* (the params' FUSED / WAVEFRONT flags win) [0..2] */
-    uint64_t fused_max_paths;       /* AUTO rule: fused for tiles of <= this many paths, 2^24       */
+    uint64_t fused_max_paths;       /* AUTO rule: fused for tiles of <= this many paths, 2^25       */
     uint32_t wavefront_paths;       /* paths in flight when params.wavefront_paths == 0, 2^25 [1..2^31) */
     uint32_t streams;               /* sub-wavefronts (HIP streams) of the wavefront, 4      [1..4] */
     uint32_t isect_refill_idle;     /* refill a wave once this many lanes are idle, 24       [1..64] */

@@ -686,7 +686,7 @@ void spt_default_config(spt_config* c) {
     c->ploc_radius = 16;
     c->stack_slack = 0;
     c->pipeline = SPT_PIPELINE_AUTO;
-    c->fused_max_paths = 1ull << 24;
+    c->fused_max_paths = 1ull << 25;
     c->wavefront_paths = 1u << 25;
     c->streams = 4;
     c->isect_refill_idle = 24;
@@ -1337,10 +1337,13 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // fused 2308 vs wavefront 1982 Mpaths/s; whole image: 2353 vs 2825.
     // Traversal counters exist in the wavefront isect kernel only.
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
-    // the job-size rule: the fused kernel up to fused_max_paths = 16M paths
-    // (config 1 tiles: 1/4 fused 3559 vs wavefront 3224, 1/8 3078 vs 2448
-    // Mpaths/s; whole image 3848 vs 3823, within noise, so the wavefront keeps
-    // large jobs); an explicit wavefront size moves the rule with it
+    // the job-size rule: the fused kernel up to fused_max_paths = 32M paths,
+    // one rank's share of config 1 at N >= 2 (tiles 1/2, 1/4, 1/8: fused 4393,
+    // 4187, 3667 vs wavefront 4220, 3572, 2622 Mpaths/s; config 4's tiles
+    // 1/2-1/8 fused 750-788 vs 684-713); the whole config-1 image, 4577 vs
+    // 4505, is within run-to-run noise, so the north-star wavefront keeps the
+    // single-GPU job (profiles/r02_thr/); an explicit wavefront size moves the
+    // rule with it
     const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : cfg.fused_max_paths;
     bool fused = cfg.pipeline == SPT_PIPELINE_AUTO ? P * p.spp <= fused_max : cfg.pipeline == SPT_PIPELINE_FUSED;
     if (p.flags & SPT_FLAG_FUSED) fused = true;

@@ -160,7 +160,7 @@ def test_config_defaults_and_env_overrides():
     c = sptamd.default_config()
     assert (c.build, c.bvh_width, c.collapse, c.ploc_radius) == (0, 6, 0, 16)
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
-    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 24      # spt.h docs = code
+    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 25      # spt.h docs = code
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
     assert c.pack_groups == 1
     e = sptamd.config_from_env(environ={"SPT_STREAMS": "2", "SPT_BUILD": "gpu", "SPT_FUSED": "0",
