@@ -115,6 +115,7 @@ struct Workspace {
     PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
     Stats* stats = nullptr;
+    Stats* host_stats = nullptr;        // pinned readback of stats
     hipEvent_t fork_ev = nullptr;
     std::vector<hipEvent_t> events;
 
@@ -127,6 +128,7 @@ struct Workspace {
             if (b.stream) (void)hipStreamDestroy(b.stream);
         }
         hfree(film); hfree(acc); hfree(jumps); hfree(stats);
+        if (host_stats) (void)hipHostFree(host_stats);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         for (auto e : events) (void)hipEventDestroy(e);
         *this = Workspace();
@@ -270,6 +272,7 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, u
         ws.jump_cap = njumps;
     }
     if (!ws.stats) HIP_TRY(hipMalloc((void**)&ws.stats, sizeof(Stats)));
+    if (!ws.host_stats) HIP_TRY(hipHostMalloc((void**)&ws.host_stats, sizeof(Stats), hipHostMallocDefault));
     if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
     return SPT_OK;
 }
@@ -1642,8 +1645,10 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         }
         if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
     }
-    unsigned long long hstats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    HIP_TRY(hipMemcpyAsync(hstats, ws.stats, sizeof(hstats), hipMemcpyDeviceToHost, stream));
+    // pinned destination: a pageable one makes the copy a staged, slower transfer
+    const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(ws.host_stats);
+    static_assert(sizeof(Stats) == 8 * sizeof(unsigned long long), "Stats is the 8 counters read back here");
+    HIP_TRY(hipMemcpyAsync(ws.host_stats, ws.stats, sizeof(Stats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
     rs.continuations = hstats[1];

@@ -194,3 +194,27 @@ def test_library_reads_no_environment():
     assert len(srcs) > 10
     for f in srcs:
         assert not re.search(r"\b(getenv|secure_getenv)\s*\(", open(f).read()), f
+
+
+def test_tile_row_count_matches_library():
+    """The Python host's closed-form row count (used on every render) equals spt_tile_rows."""
+    from sptamd import _lib
+    for h in (0, 1, 7, 40, 1000, 1024, 1080):
+        for tc in (0, 1, 2, 3, 8):
+            for rpg in (0, 1, 4, 8, 64):
+                for ti in range(tc + 1):
+                    assert _lib.tile_row_count(h, ti, tc, rpg) == _lib.lib.spt_tile_rows(h, ti, tc, rpg, None, 0), \
+                        (h, ti, tc, rpg)
+
+
+def test_env_snapshot_tracks_environment(monkeypatch):
+    """sync_config's cheap env read sees every change made through os.environ."""
+    from sptamd import _lib
+    i = list(_lib._ENV_CONFIG).index("SPT_STREAMS")
+    monkeypatch.delenv("SPT_STREAMS", raising=False)
+    assert _lib.env_snapshot()[i] is None
+    monkeypatch.setenv("SPT_STREAMS", "3")
+    assert _lib.env_snapshot()[i] == "3" and _lib.config_from_env().streams == 3
+    monkeypatch.setenv("SPT_STREAMS", "")
+    assert _lib.config_from_env().streams == _lib.default_config().streams
+    assert _lib.env_snapshot({"SPT_STREAMS": "2"})[i] == "2"
