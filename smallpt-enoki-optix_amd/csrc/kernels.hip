@@ -10,6 +10,21 @@
 
 namespace spt {
 
+// A wave-uniform value (every lane active and holding the same value) as a
+// scalar: the compiler cannot tell that threadIdx.x >> 6 or a value shuffled
+// from lane 0 is uniform, and would otherwise keep the work-pool state in
+// VGPRs and branch on it per lane.
+#ifndef SPT_UNIFORM
+#define SPT_UNIFORM 1
+#endif
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
+#if SPT_UNIFORM
+    return __builtin_amdgcn_readfirstlane(v);
+#else
+    return v;
+#endif
+}
+
 // minimum waves per SIMD the isect kernels are compiled for (register budget)
 #ifndef SPT_ISECT_WAVES
 #define SPT_ISECT_WAVES 1
@@ -643,7 +658,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
     // wave-uniform pool state
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
     const uint32_t blk = a.xcd_remap ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
-    const uint32_t wave_id = blk * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wave_id = wave_uniform(blk * (kIsectBlock / 64) + (threadIdx.x >> 6));
     const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
     const uint32_t dyn_base = share * nwaves;
     uint32_t pool = wave_id * share, pool_end = pool + share;
@@ -657,7 +672,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
                 if (pool == pool_end) {
                     uint32_t base = 0;
                     if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, a.chunk);
-                    base = dyn_base + (uint32_t)__shfl((int)base, 0);
+                    base = dyn_base + wave_uniform((uint32_t)__shfl((int)base, 0));
                     if (base >= n) { drained = true; break; }
                     pool = base;
                     pool_end = min(base + a.chunk, n);
@@ -745,7 +760,7 @@ void isect_public_persistent_kernel(IsectPublicArgs a) {
     uint32_t ray = 0;
     bool busy = false;
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
-    const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wave_id = wave_uniform(blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6));
     const uint32_t share = (uint32_t)(((uint64_t)a.n + nwaves - 1) / nwaves);
     uint32_t pool = min(a.n, wave_id * share);
     const uint32_t pool_end = min(a.n, pool + share);
@@ -1080,7 +1095,7 @@ void render_fused_kernel(FusedArgs a) {
     uint32_t casts = 0, conts = 0, starts = 0;
     // wave-uniform work pool: static share, then dynamic chunks
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
-    const uint32_t wave_id = blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wave_id = wave_uniform(blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6));
     const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
     const uint32_t dyn_base = share * nwaves;
     uint32_t pool = wave_id * share, pool_end = pool + share;
@@ -1178,7 +1193,7 @@ void render_fused_kernel(FusedArgs a) {
                 if (pool == pool_end) {
                     uint32_t base = 0;
                     if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, a.chunk);
-                    base = dyn_base + (uint32_t)__shfl((int)base, 0);
+                    base = dyn_base + wave_uniform((uint32_t)__shfl((int)base, 0));
                     if (base >= n) { drained = true; break; }
                     pool = base;
                     pool_end = min(base + a.chunk, n);
