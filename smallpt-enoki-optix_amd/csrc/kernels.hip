@@ -917,11 +917,22 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 
     // ---- phase 1: survive or terminate (the bounce inputs load alongside)
     bool emit = false;
-    uint32_t pix = 0, meta = 0, gpix = 0, kind = kMatDiffuse;
+    uint32_t pix = 0, meta = 0, kind = kMatDiffuse;
     int32_t slot = -1;
-    float4 hit = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m0 = hit, m1 = hit, m2 = hit;
+    // The bounce inputs (hit, m0-m2, o, d, gpix) are read only where they were
+    // set (phase 2 runs for survivors, emit); left uninitialised the compiler
+    // materialises no zeros for them at every join (~45 VALU moves per
+    // thread, issue slots the co-running isect grids want).  With spheres a
+    // sphere hit keeps m0-m2 at zero on purpose (scatter ignores them).
+    uint32_t gpix;
+    float4 hit, m0, m1, m2;
+    V3 o, d;
+    if constexpr (kSpt) {
+        gpix = 0;
+        hit = m0 = m1 = m2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        o = d = v3(0, 0, 0);
+    }
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
-    V3 o = v3(0, 0, 0), d = v3(0, 0, 0);
     if (i < n) {
         const float4 q1 = a.in.q1[i], q2 = a.in.q2[i];
         meta = f2u(q1.w);
@@ -972,7 +983,9 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             if (kMode == kModeUnit) {
                 term = !bounce;  // albedo 1: the throughput stays 1, roulette never fires
             } else {
-                uint32_t mat = sph ? (a.sc.sph_mat ? (uint32_t)a.sc.sph_mat[-2 - slot] : 0u) : f2u(m0.w);
+                uint32_t mat = 0;  // (m0 was loaded iff emitters or a bounce need it)
+                if (sph) mat = a.sc.sph_mat ? (uint32_t)a.sc.sph_mat[-2 - slot] : 0u;
+                else if (kMode == kModeEmit || bounce) mat = f2u(m0.w);
                 if (kSpt) kind = material_kind(a.sc, mat);
                 if (kMode == kModeEmit && mat < a.sc.nemit) {
                     // emitted radiance at the hit (smallpt obj.e; not in the reference)
@@ -1034,7 +1047,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     }
 
     // ---- phase 2: the bounce ray of every survivor
-    V3 no = v3(0, 0, 0), nd = v3(0, 0, 0);
+    V3 no, nd;
     if (emit) {
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
