@@ -221,6 +221,10 @@ typedef struct spt_config {
     /* --- scene build, continued */
     uint32_t pack_groups;           /* 1: wide-BVH child groups packed into each other's empty
                                        slots (denser node lines), 0: eight aligned slots each [0..1] */
+    /* --- spt_render, continued */
+    uint32_t pixel_block;           /* camera paths start in B x B pixel blocks, 0 (0 or 1:
+                                       scanline, measured fastest: DESIGN.md §4); the image
+                                       does not depend on it                             [0..64] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

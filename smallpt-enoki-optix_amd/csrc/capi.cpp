@@ -325,6 +325,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(public_persistent, 0, 1)
     CFG_RANGE(public_refill_idle, 1, 64)
     CFG_RANGE(pack_groups, 0, 1)
+    CFG_RANGE(pixel_block, 0, 64)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -705,6 +706,7 @@ void spt_default_config(spt_config* c) {
     c->public_persistent = 0;
     c->public_refill_idle = kRefillIdle;
     c->pack_groups = 1;
+    c->pixel_block = 0;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1477,6 +1479,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         R.stats = ws.stats->stats;
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
+        R.pixel_block = cfg.pixel_block;
         R.initstate = p.rng_initstate;
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
@@ -1496,6 +1499,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.P = (uint32_t)P; F.W = p.width; F.max_depth = p.max_depth;
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
         F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
+        F.pixel_block = cfg.pixel_block;
         F.refill_idle = cfg.fused_refill_idle;
         // a small static share: the fused lanes' path lengths vary far more
         // than one cast's, so most work is taken dynamically (1/8 tile of

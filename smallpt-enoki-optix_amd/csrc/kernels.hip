@@ -878,8 +878,9 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     if (i >= total) return;
     const uint64_t w = cur + i;
     const uint32_t s = (uint32_t)(w / a.P);
-    const uint32_t p = (uint32_t)(w - (uint64_t)s * a.P);
-    const uint32_t lx = p % a.W, ly = p / a.W;
+    uint32_t lx, ly;
+    work_pixel((uint32_t)(w - (uint64_t)s * a.P), a.W, a.P, a.pixel_block, lx, ly);
+    const uint32_t p = ly * a.W + lx;
     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
     const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
     Pcg32 rng;
@@ -1217,8 +1218,9 @@ void render_fused_kernel(FusedArgs a) {
                 if (!busy && !pending && rank < take) {
                     const uint64_t wk = a.work0 + pool + rank;
                     sample = (uint32_t)(wk / a.P);
-                    pix = (uint32_t)(wk - (uint64_t)sample * a.P);
-                    const uint32_t lx = pix % a.W, ly = pix / a.W;
+                    uint32_t lx, ly;
+                    work_pixel((uint32_t)(wk - (uint64_t)sample * a.P), a.W, a.P, a.pixel_block, lx, ly);
+                    pix = ly * a.W + lx;
                     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
                     gpix = gy * a.W + lx;                          // main.cpp:379-382
                     Pcg32 rng;

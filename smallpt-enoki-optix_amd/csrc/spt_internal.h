@@ -266,6 +266,7 @@ struct RefillArgs {
     uint64_t work_end;          // W_total (work items of this chunk end here)
     uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
+    uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
     uint64_t initstate;
     int mode;                   // PathMode: which planes a new path fills
 };
@@ -284,6 +285,7 @@ struct FusedArgs {
     uint64_t work0, initstate;
     uint32_t count, P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
+    uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
     uint32_t refill_idle, static_share_q8, chunk, grid_q8;
     float env_r, env_g, env_b;
 };
@@ -305,6 +307,27 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
                                 uint32_t rows_per_group) {
     uint32_t g = local_row / rows_per_group;
     return (g * tile_count + tile_index) * rows_per_group + local_row % rows_per_group;
+}
+
+// Tile pixel of the q-th camera path of a sample (q in [0, P), P = W * H):
+// row bands of B rows, each cut into B-wide blocks taken in order, q running
+// row-major inside a block (the last band / block may be shorter).  A wave's
+// 64 consecutive camera paths then cover an 8 x 8 footprint instead of 64
+// pixels of one row (B = 8), and bounce rays inherit that locality through
+// the order-preserving compaction.  Any B covers every pixel once, so the
+// image does not depend on it.  B <= 1: scanline order.
+SPT_HD void work_pixel(uint32_t q, uint32_t W, uint32_t P, uint32_t B, uint32_t& lx, uint32_t& ly) {
+    if (B <= 1) { lx = q % W; ly = q / W; return; }
+    const uint32_t H = P / W;
+    const uint32_t band = q / (B * W);
+    const uint32_t off = q - band * B * W;
+    const uint32_t rb = H - band * B < B ? H - band * B : B;
+    const uint32_t cb = off / (B * rb);
+    const uint32_t inner = off - cb * B * rb;
+    const uint32_t cw = W - cb * B < B ? W - cb * B : B;
+    const uint32_t r = inner / cw;
+    lx = cb * B + (inner - r * cw);
+    ly = band * B + r;
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);

@@ -261,6 +261,31 @@ def test_film_chunking_bitexact(small, pipeline, streams, per_chunk, mode):
     assert st["streams"] == (1 if pipeline == "fused" else streams)
 
 
+@pytest.mark.parametrize("pipeline", ["wavefront", "fused"])
+@pytest.mark.parametrize("block", [0, 1, 3, 4, 8, 64])
+def test_pixel_block_bitexact(small, pipeline, block):
+    """spt_config.pixel_block (camera paths in B x B pixel blocks) changes the
+    order work starts in, never the image: bit-equal to the oracle on a tile
+    whose sides are not multiples of B, and on an interleaved row tile."""
+    m, albedo, osc = small
+    w, h, spp, depth = 37, 29, 5, 4
+    cfg = sptamd.default_config()
+    cfg.pixel_block = block
+    s = sptamd.Scene(config=cfg)
+    s.add_arrays(m)
+    s.commit(0)
+    s.backend.set_albedo(albedo)
+    got, st = render(s, w, h, spp, depth, pipeline=pipeline, wavefront_paths=1000, rr_start_depth=2)
+    ref, casts = osc.render(O.reference_params(w, h, spp, depth, rr_start_depth=2))
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+    # rank 1 of 3 with 4-row groups: the tile's own (shorter) block rows
+    tile, _ = render(s, w, h, spp, depth, pipeline=pipeline, wavefront_paths=1000, rr_start_depth=2,
+                     tile_index=1, tile_count=3, rows_per_group=4)
+    rows = [r for r in range(h) if (r // 4) % 3 == 1]
+    np.testing.assert_array_equal(tile, ref[:, rows, :])
+
+
 def test_config_through_the_abi(small, monkeypatch):
     """Knobs set through spt_config (no environment variable anywhere) change
     scheduling only; invalid values are rejected by spt_scene_set_config."""
