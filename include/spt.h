@@ -225,6 +225,9 @@ typedef struct spt_config {
     uint32_t pixel_block;           /* camera paths start in B x B pixel blocks, 0 (0 or 1:
                                        scanline, measured fastest: DESIGN.md §4); the image
                                        does not depend on it                             [0..64] */
+    uint32_t work_order;            /* 0: work items sample-major (every pixel of a sample, then
+                                       the next sample), 1: pixel-major (a pixel's samples
+                                       together); the image does not depend on it   [0..1] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

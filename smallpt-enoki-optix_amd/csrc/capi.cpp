@@ -326,6 +326,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(public_refill_idle, 1, 64)
     CFG_RANGE(pack_groups, 0, 1)
     CFG_RANGE(pixel_block, 0, 64)
+    CFG_RANGE(work_order, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -707,6 +708,7 @@ void spt_default_config(spt_config* c) {
     c->public_refill_idle = kRefillIdle;
     c->pack_groups = 1;
     c->pixel_block = 0;
+    c->work_order = 0;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1405,8 +1407,9 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const auto resolve = [&](uint32_t s0, uint32_t ns) {
         return mode == kModeUnit
                    ? launch_resolve_flags(sflag, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                          p.env[0], p.env[1], p.env[2], stream)
-                   : launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp, stream);
+                                          p.env[0], p.env[1], p.env[2], cfg.work_order, stream)
+                   : launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
+                                    cfg.work_order, stream);
     };
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
@@ -1472,6 +1475,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         S.xcd_remap = (cfg.xcd_remap >> 1) & 1u;
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
         S.tile_index = p.tile_index; S.tile_count = p.tile_count; S.rows_per_group = p.rows_per_group;
+        S.work_order = cfg.work_order;
         S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];
         RefillArgs& R = ra[k];
         R.cam = cam;
@@ -1480,6 +1484,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
         R.pixel_block = cfg.pixel_block;
+        R.work_order = cfg.work_order;
         R.initstate = p.rng_initstate;
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
@@ -1500,6 +1505,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
         F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
         F.pixel_block = cfg.pixel_block;
+        F.work_order = cfg.work_order;
         F.refill_idle = cfg.fused_refill_idle;
         // a small static share: the fused lanes' path lengths vary far more
         // than one cast's, so most work is taken dynamically (1/8 tile of
@@ -1514,6 +1520,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             F.work0 = (uint64_t)s0 * P;
             F.count = (uint32_t)((uint64_t)ns * P);  // <= 4 GiB / 12 B per chunk
             F.sample0 = s0;
+            F.chunk_ns = ns;
             HIP_TRY(hipMemsetAsync(F.next, 0, sizeof(uint32_t), stream));
             if ((st = mark(1, stream, [&] { return launch_fused(F, mode, stream, &lanes); }))) return st;
             if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
@@ -1535,7 +1542,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             const uint64_t wb = w0 + L * k / K, we = w0 + L * (k + 1) / K;
             HIP_TRY(hipMemsetAsync(b.cnt, 0, sizeof(Counters), strm[k]));
             ra[k].work_end = we;
-            sa[k].sample0 = s0;
+            ra[k].chunk_s0 = s0; ra[k].chunk_ns = ns;
+            sa[k].sample0 = s0; sa[k].chunk_ns = ns;
             // the first refill starts at the sub-wavefront's first work item
             ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = nullptr; ra[k].cursor_init = wb;
             ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];

@@ -876,10 +876,9 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
     }
     if (i >= total) return;
-    const uint64_t w = cur + i;
-    const uint32_t s = (uint32_t)(w / a.P);
-    uint32_t lx, ly;
-    work_pixel((uint32_t)(w - (uint64_t)s * a.P), a.W, a.P, a.pixel_block, lx, ly);
+    uint32_t s, q, lx, ly;
+    work_item(cur + i, a.chunk_s0, a.chunk_ns, a.P, a.work_order, s, q);
+    work_pixel(q, a.W, a.P, a.pixel_block, lx, ly);
     const uint32_t p = ly * a.W + lx;
     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
     const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
@@ -896,7 +895,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 // writes its contribution once per (sample, pixel): unit mode one byte
 // (escaped or not: the sky term is added in sample order by the resolve),
 // otherwise its gathered radiance (throughput x sky radiance on escape, plus
-// emitted radiance with emitters) to sfilm[sample][c][pixel].  Survivors are
+// emitted radiance with emitters) to its film slot (film_slot / film_rgb).  Survivors are
 // compacted into the out queue with a wave ballot + mbcnt rank and one
 // atomicAdd per block.  Phase 1 decides which paths survive (miss, last cast,
 // albedo, roulette) from the hit and the material word alone, so the block's
@@ -1017,12 +1016,13 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         emit = !term;
         if (term) {
             if (kMode == kModeUnit) {
-                a.sflag[(size_t)(sample - a.sample0) * a.P + pix] = escaped ? 1 : 0;
+                a.sflag[film_slot(sample - a.sample0, pix, a.P, a.chunk_ns, a.work_order)] = escaped ? 1 : 0;
             } else {
-                float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
+                size_t cs;
+                float* f = film_rgb(a.sfilm, sample - a.sample0, pix, a.P, a.chunk_ns, a.work_order, cs);
                 f[0] = lr;
-                f[(size_t)a.P] = lg;
-                f[(size_t)2 * a.P] = lb;
+                f[cs] = lg;
+                f[2 * cs] = lb;
             }
         }
     }
@@ -1192,12 +1192,13 @@ void render_fused_kernel(FusedArgs a) {
                 }
                 if (term) {
                     if (kMode == kModeUnit) {
-                        a.sflag[(size_t)(sample - a.sample0) * a.P + pix] = slot == -1 ? 1 : 0;
+                        a.sflag[film_slot(sample - a.sample0, pix, a.P, a.chunk_ns, a.work_order)] = slot == -1 ? 1 : 0;
                     } else {
-                        float* f = a.sfilm + (size_t)(sample - a.sample0) * 3 * a.P + pix;
+                        size_t cs;
+                        float* f = film_rgb(a.sfilm, sample - a.sample0, pix, a.P, a.chunk_ns, a.work_order, cs);
                         f[0] = lr;
-                        f[(size_t)a.P] = lg;
-                        f[(size_t)2 * a.P] = lb;
+                        f[cs] = lg;
+                        f[2 * cs] = lb;
                     }
                 }
             }
@@ -1216,10 +1217,9 @@ void render_fused_kernel(FusedArgs a) {
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
                 if (!busy && !pending && rank < take) {
-                    const uint64_t wk = a.work0 + pool + rank;
-                    sample = (uint32_t)(wk / a.P);
-                    uint32_t lx, ly;
-                    work_pixel((uint32_t)(wk - (uint64_t)sample * a.P), a.W, a.P, a.pixel_block, lx, ly);
+                    uint32_t q, lx, ly;
+                    work_item(a.work0 + pool + rank, a.sample0, a.chunk_ns, a.P, a.work_order, sample, q);
+                    work_pixel(q, a.W, a.P, a.pixel_block, lx, ly);
                     pix = ly * a.W + lx;
                     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
                     gpix = gy * a.W + lx;                          // main.cpp:379-382
@@ -1269,12 +1269,16 @@ void render_fused_kernel(FusedArgs a) {
 // Chunks of samples carry the running sum in acc.
 __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ sfilm, float* __restrict__ acc,
                                                       float* __restrict__ out, uint32_t P, uint32_t nsamples,
-                                                      uint32_t first_chunk, uint32_t last_chunk, uint32_t spp) {
+                                                      uint32_t first_chunk, uint32_t last_chunk, uint32_t spp,
+                                                      uint32_t order) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= P) return;
     for (uint32_t c = 0; c < 3; c++) {
         float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
-        for (uint32_t s = 0; s < nsamples; s++) sum = sum + sfilm[((size_t)s * 3 + c) * P + p];
+        for (uint32_t s = 0; s < nsamples; s++) {
+            size_t cs;
+            sum = sum + film_rgb(const_cast<float*>(sfilm), s, p, P, nsamples, order, cs)[c * cs];
+        }
         if (last_chunk)
             out[(size_t)c * P + p] = sum / (float)spp;
         else
@@ -1290,11 +1294,11 @@ __global__ __launch_bounds__(256) void resolve_flags_kernel(const uint8_t* __res
                                                             float* __restrict__ acc, float* __restrict__ out,
                                                             uint32_t P, uint32_t nsamples, uint32_t first_chunk,
                                                             uint32_t last_chunk, uint32_t spp, float env_r,
-                                                            float env_g, float env_b) {
+                                                            float env_g, float env_b, uint32_t order) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= P) return;
     uint32_t k = 0;
-    for (uint32_t s = 0; s < nsamples; s++) k += sflag[(size_t)s * P + p];
+    for (uint32_t s = 0; s < nsamples; s++) k += sflag[film_slot(s, p, P, nsamples, order)];
     const float env[3] = {env_r, env_g, env_b};
     for (uint32_t c = 0; c < 3; c++) {
         float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
@@ -1524,19 +1528,19 @@ hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s
 }
 
 hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
-                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, hipStream_t s) {
+                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, uint32_t order, hipStream_t s) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(resolve_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sfilm, acc, out, P, nsamples,
-                       first_chunk, last_chunk, spp);
+                       first_chunk, last_chunk, spp, order);
     return hipGetLastError();
 }
 
 hipError_t launch_resolve_flags(const uint8_t* sflag, float* acc, float* out, uint32_t P, uint32_t nsamples,
                                 uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, float env_r, float env_g,
-                                float env_b, hipStream_t s) {
+                                float env_b, uint32_t order, hipStream_t s) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(resolve_flags_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sflag, acc, out, P, nsamples,
-                       first_chunk, last_chunk, spp, env_r, env_g, env_b);
+                       first_chunk, last_chunk, spp, env_r, env_g, env_b, order);
     return hipGetLastError();
 }
 

@@ -243,6 +243,7 @@ struct ShadeArgs {
     uint64_t initstate;
     uint32_t P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
+    uint32_t work_order, chunk_ns;  // film layout follows the work order (film_slot)
     float env_r, env_g, env_b;
     uint32_t xcd_remap;         // 1: blocks sharing an XCD take adjacent slot ranges
 };
@@ -267,6 +268,8 @@ struct RefillArgs {
     uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
+    uint32_t work_order;        // 0: sample-major work items, 1: pixel-major inside the chunk
+    uint32_t chunk_s0, chunk_ns;  // the chunk's first sample and sample count
     uint64_t initstate;
     int mode;                   // PathMode: which planes a new path fills
 };
@@ -286,6 +289,7 @@ struct FusedArgs {
     uint32_t count, P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
     uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
+    uint32_t work_order, chunk_ns;  // 1: pixel-major work items (chunk of chunk_ns samples)
     uint32_t refill_idle, static_share_q8, chunk, grid_q8;
     float env_r, env_g, env_b;
 };
@@ -316,6 +320,36 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
 // pixels of one row (B = 8), and bounce rays inherit that locality through
 // the order-preserving compaction.  Any B covers every pixel once, so the
 // image does not depend on it.  B <= 1: scanline order.
+// Work item w of the chunk of samples [s0, s0 + ns) -> (sample, pixel-order
+// index q).  Sample-major (order 0): w = s * P + q, so the paths in flight
+// cover a few samples of the whole tile.  Pixel-major (order 1): a pixel's ns
+// samples are consecutive work items, so a wave starts 64 samples of one
+// pixel and a contiguous share of the queue covers a band of the tile.  Both
+// cover every (sample, pixel) of the chunk once.
+SPT_HD void work_item(uint64_t w, uint32_t s0, uint32_t ns, uint32_t P, uint32_t order, uint32_t& s, uint32_t& q) {
+    if (order == 0) {
+        s = (uint32_t)(w / P);
+        q = (uint32_t)(w - (uint64_t)s * P);
+        return;
+    }
+    const uint32_t local = (uint32_t)(w - (uint64_t)s0 * P);
+    q = local / ns;
+    s = s0 + (local - q * ns);
+}
+
+// Per-(sample, pixel) film slot of a chunk of ns samples: [sample][pixel] for
+// sample-major work, [pixel][sample] for pixel-major work, so the paths a wave
+// ends together write neighbouring slots either way.  The RGB film (albedo /
+// emit modes) keeps three floats per slot: channel stride P or 1 (film_rgb).
+SPT_HD size_t film_slot(uint32_t sl, uint32_t pix, uint32_t P, uint32_t ns, uint32_t order) {
+    return order ? (size_t)pix * ns + sl : (size_t)sl * P + pix;
+}
+SPT_HD float* film_rgb(float* sfilm, uint32_t sl, uint32_t pix, uint32_t P, uint32_t ns, uint32_t order,
+                       size_t& stride) {
+    stride = order ? 1 : P;
+    return order ? sfilm + ((size_t)pix * ns + sl) * 3 : sfilm + (size_t)sl * 3 * P + pix;
+}
+
 SPT_HD void work_pixel(uint32_t q, uint32_t W, uint32_t P, uint32_t B, uint32_t& lx, uint32_t& ly) {
     if (B <= 1) { lx = q % W; ly = q / W; return; }
     const uint32_t H = P / W;
@@ -337,11 +371,11 @@ hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* l
 hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
-                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, hipStream_t s);
+                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, uint32_t order, hipStream_t s);
 // unit mode: film = env added once per escaped sample, in sample order
 hipError_t launch_resolve_flags(const uint8_t* sflag, float* acc, float* out, uint32_t P, uint32_t nsamples,
                                 uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, float env_r, float env_g,
-                                float env_b, hipStream_t s);
+                                float env_b, uint32_t order, hipStream_t s);
 hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s);
 
 }  // namespace spt

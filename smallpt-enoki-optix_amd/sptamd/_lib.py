@@ -111,7 +111,7 @@ class Config(ctypes.Structure):
                 ("fused_refill_idle", c_uint32), ("fused_static_share_q8", c_uint32), ("fused_grid_q8", c_uint32),
                 ("plane_pad", c_uint32), ("film_budget_bytes", c_uint64),
                 ("public_persistent", c_uint32), ("public_refill_idle", c_uint32), ("pack_groups", c_uint32),
-                ("pixel_block", c_uint32)]
+                ("pixel_block", c_uint32), ("work_order", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -227,6 +227,7 @@ _ENV_CONFIG = {
     "SPT_PUBLIC_REFILL_IDLE": ("public_refill_idle", int),
     "SPT_PACK": ("pack_groups", int),
     "SPT_PIXEL_BLOCK": ("pixel_block", int),
+    "SPT_WORK_ORDER": ("work_order", int),
 }
 
 

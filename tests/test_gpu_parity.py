@@ -262,15 +262,21 @@ def test_film_chunking_bitexact(small, pipeline, streams, per_chunk, mode):
 
 
 @pytest.mark.parametrize("pipeline", ["wavefront", "fused"])
-@pytest.mark.parametrize("block", [0, 1, 3, 4, 8, 64])
-def test_pixel_block_bitexact(small, pipeline, block):
-    """spt_config.pixel_block (camera paths in B x B pixel blocks) changes the
-    order work starts in, never the image: bit-equal to the oracle on a tile
-    whose sides are not multiples of B, and on an interleaved row tile."""
+@pytest.mark.parametrize("block,order,per_chunk", [(0, 0, 0), (1, 0, 0), (3, 0, 0), (4, 0, 0), (8, 0, 0), (64, 0, 0),
+                                                   (0, 1, 0), (3, 1, 0), (0, 1, 2), (4, 1, 2), (0, 0, 2)])
+def test_work_order_bitexact(small, pipeline, block, order, per_chunk):
+    """spt_config.pixel_block (camera paths in B x B pixel blocks) and
+    work_order (sample- or pixel-major work items, with 2-sample film chunks
+    too) change the order work starts in, never the image: bit-equal to the
+    oracle on a tile whose sides are not multiples of B, and on an interleaved
+    row tile."""
     m, albedo, osc = small
     w, h, spp, depth = 37, 29, 5, 4
     cfg = sptamd.default_config()
     cfg.pixel_block = block
+    cfg.work_order = order
+    if per_chunk:
+        cfg.film_budget_bytes = 12 * w * h * per_chunk
     s = sptamd.Scene(config=cfg)
     s.add_arrays(m)
     s.commit(0)
@@ -284,6 +290,13 @@ def test_pixel_block_bitexact(small, pipeline, block):
                      tile_index=1, tile_count=3, rows_per_group=4)
     rows = [r for r in range(h) if (r // 4) % 3 == 1]
     np.testing.assert_array_equal(tile, ref[:, rows, :])
+    # unit mode (albedo 1: one escape byte per film slot)
+    u = sptamd.Scene(config=cfg)
+    u.add_arrays(m)
+    u.commit(0)
+    got_u, _ = render(u, w, h, spp, depth, pipeline=pipeline, wavefront_paths=1000)
+    ref_u, _ = O.OracleScene(m).render(O.reference_params(w, h, spp, depth))
+    np.testing.assert_array_equal(got_u, ref_u)
 
 
 def test_config_through_the_abi(small, monkeypatch):
