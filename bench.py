@@ -309,6 +309,9 @@ def main():
         # render_fused_kernel, whose only HBM stream is the per-sample film
         # write (12 B per path; rays stay in registers).
         fused = bool(st.get("fused"))
+        wo = scene.backend.config["work_order"]
+        work_order = {1: "sample-major", 2: "pixel-major"}.get(wo) or (
+            ("pixel-major" if sstats["device_bytes"] >= 4 << 20 else "sample-major") + " (auto)")
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
         casts_per_launch = agg["ray_casts"] / launches
@@ -357,6 +360,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
+            "work_order_rule": "auto: pixel-major for scenes of >= 4 MiB on the device, else sample-major "
+                               "(DESIGN.md §4)",
             "pipeline_rule": "auto: fused for tiles of <= 32M paths, else wavefront (DESIGN.md §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
@@ -364,7 +369,8 @@ def main():
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
-                       "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4)},
+                       "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4),
+                       "work_order": work_order},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",

@@ -190,6 +190,11 @@ enum {
     SPT_PIPELINE_WAVEFRONT = 1, /* isect / shade / refill over path queues */
     SPT_PIPELINE_FUSED = 2      /* one persistent trace+shade kernel per sample chunk */
 };
+enum {
+    SPT_WORK_AUTO = 0,
+    SPT_WORK_SAMPLE_MAJOR = 1,
+    SPT_WORK_PIXEL_MAJOR = 2
+};
 typedef struct spt_config {
     /* --- scene build (spt_scene_create_cfg) */
     uint32_t build;                 /* spt_build (AUTO: GPU from gpu_build_min_tris up)      [0..2] */
@@ -225,9 +230,11 @@ typedef struct spt_config {
     uint32_t pixel_block;           /* camera paths start in B x B pixel blocks, 0 (0 or 1:
                                        scanline, measured fastest: DESIGN.md §4); the image
                                        does not depend on it                             [0..64] */
-    uint32_t work_order;            /* 0: work items sample-major (every pixel of a sample, then
-                                       the next sample), 1: pixel-major (a pixel's samples
-                                       together); the image does not depend on it   [0..1] */
+    uint32_t work_order;            /* SPT_WORK_*: the order paths start in — sample-major (every
+                                       pixel of a sample, then the next sample) or pixel-major (a
+                                       pixel's samples together); AUTO: pixel-major for scenes of
+                                       >= 4 MiB on the device; the image does
+                                       not depend on it                                  [0..2] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -326,7 +326,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(public_refill_idle, 1, 64)
     CFG_RANGE(pack_groups, 0, 1)
     CFG_RANGE(pixel_block, 0, 64)
-    CFG_RANGE(work_order, 0, 1)
+    CFG_RANGE(work_order, 0, SPT_WORK_PIXEL_MAJOR)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -708,7 +708,7 @@ void spt_default_config(spt_config* c) {
     c->public_refill_idle = kRefillIdle;
     c->pack_groups = 1;
     c->pixel_block = 0;
-    c->work_order = 0;
+    c->work_order = SPT_WORK_AUTO;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1355,6 +1355,13 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     bool fused = cfg.pipeline == SPT_PIPELINE_AUTO ? P * p.spp <= fused_max : cfg.pipeline == SPT_PIPELINE_FUSED;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
     if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
+    // Work order (spt_config.work_order).  AUTO: pixel-major once the scene
+    // outgrows an XCD's L2 — the paths in flight then cover a band of the
+    // tile, whose scene working set is smaller (config 3 +26 %, fused config
+    // 1 +7 %, config 4 +3 %, wavefront config 1 +0.4 %); a scene that fits has
+    // nothing to gain (config 2 -4.6 %; profiles/r02_workorder).
+    const uint32_t pixel_major = cfg.work_order == SPT_WORK_PIXEL_MAJOR ||
+                                 (cfg.work_order == SPT_WORK_AUTO && sc->stats.device_bytes >= kPixelMajorMinSceneBytes);
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);
@@ -1404,12 +1411,14 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     float* sfilm = (float*)ws.film;
     uint8_t* sflag = (uint8_t*)ws.film;
     float* acc = ws.acc;
+    // film slots follow the work order (film_slot)
+    const uint32_t film_order = pixel_major;
     const auto resolve = [&](uint32_t s0, uint32_t ns) {
         return mode == kModeUnit
                    ? launch_resolve_flags(sflag, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                          p.env[0], p.env[1], p.env[2], cfg.work_order, stream)
+                                          p.env[0], p.env[1], p.env[2], film_order, stream)
                    : launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                    cfg.work_order, stream);
+                                    film_order, stream);
     };
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
@@ -1475,7 +1484,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         S.xcd_remap = (cfg.xcd_remap >> 1) & 1u;
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
         S.tile_index = p.tile_index; S.tile_count = p.tile_count; S.rows_per_group = p.rows_per_group;
-        S.work_order = cfg.work_order;
+        S.work_order = pixel_major;
         S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];
         RefillArgs& R = ra[k];
         R.cam = cam;
@@ -1484,7 +1493,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
         R.pixel_block = cfg.pixel_block;
-        R.work_order = cfg.work_order;
+        R.work_order = pixel_major;
         R.initstate = p.rng_initstate;
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
@@ -1505,7 +1514,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
         F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
         F.pixel_block = cfg.pixel_block;
-        F.work_order = cfg.work_order;
+        F.work_order = pixel_major;
         F.refill_idle = cfg.fused_refill_idle;
         // a small static share: the fused lanes' path lengths vary far more
         // than one cast's, so most work is taken dynamically (1/8 tile of
@@ -1538,11 +1547,19 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         uint64_t started[kMaxStreams], sub_end[kMaxStreams];  // work items known started; end of the share
         for (int k = 0; k < K; k++) {
             Sub& b = ws.sub[k];
-            // contiguous share of the chunk's work items (sample-major)
-            const uint64_t wb = w0 + L * k / K, we = w0 + L * (k + 1) / K;
+            // contiguous share of the chunk's work items (sample-major); pixel-major
+            // work splits the chunk's samples instead, so that every stream
+            // covers the whole tile (a band of rows per stream would leave the
+            // streams unevenly loaded) and starts its samples of a pixel together
+            uint64_t wb = w0 + L * k / K, we = w0 + L * (k + 1) / K;
+            ra[k].chunk_s0 = s0; ra[k].chunk_ns = ns;
+            if (ra[k].work_order && ns >= (uint32_t)K) {
+                const uint32_t sk0 = s0 + ns * k / K, sk1 = s0 + ns * (k + 1) / K;
+                wb = (uint64_t)sk0 * P; we = (uint64_t)sk1 * P;
+                ra[k].chunk_s0 = sk0; ra[k].chunk_ns = sk1 - sk0;
+            }
             HIP_TRY(hipMemsetAsync(b.cnt, 0, sizeof(Counters), strm[k]));
             ra[k].work_end = we;
-            ra[k].chunk_s0 = s0; ra[k].chunk_ns = ns;
             sa[k].sample0 = s0; sa[k].chunk_ns = ns;
             // the first refill starts at the sub-wavefront's first work item
             ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = nullptr; ra[k].cursor_init = wb;

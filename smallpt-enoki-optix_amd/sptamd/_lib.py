@@ -38,6 +38,7 @@ EXPORTED = [
 ]
 SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
+SPT_WORK_AUTO, SPT_WORK_SAMPLE_MAJOR, SPT_WORK_PIXEL_MAJOR = 0, 1, 2
 
 
 class SptError(RuntimeError):

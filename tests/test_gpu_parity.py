@@ -262,12 +262,12 @@ def test_film_chunking_bitexact(small, pipeline, streams, per_chunk, mode):
 
 
 @pytest.mark.parametrize("pipeline", ["wavefront", "fused"])
-@pytest.mark.parametrize("block,order,per_chunk", [(0, 0, 0), (1, 0, 0), (3, 0, 0), (4, 0, 0), (8, 0, 0), (64, 0, 0),
-                                                   (0, 1, 0), (3, 1, 0), (0, 1, 2), (4, 1, 2), (0, 0, 2)])
+@pytest.mark.parametrize("block,order,per_chunk", [(0, 0, 0), (1, 1, 0), (3, 1, 0), (4, 0, 0), (8, 1, 0), (64, 0, 0),
+                                                   (0, 2, 0), (3, 2, 0), (0, 2, 2), (4, 2, 2), (0, 1, 2), (0, 0, 2)])
 def test_work_order_bitexact(small, pipeline, block, order, per_chunk):
     """spt_config.pixel_block (camera paths in B x B pixel blocks) and
-    work_order (sample- or pixel-major work items, with 2-sample film chunks
-    too) change the order work starts in, never the image: bit-equal to the
+    work_order (auto, sample- or pixel-major work items, with 2-sample film
+    chunks too) change the order work starts in, never the image: bit-equal to the
     oracle on a tile whose sides are not multiples of B, and on an interleaved
     row tile."""
     m, albedo, osc = small

@@ -3,7 +3,7 @@
 # pixel-major (1), config 1 wavefront and fused, configs 3 and 4.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
-E="smaj:SPT_WORK_ORDER=0 pmaj:SPT_WORK_ORDER=1"
+E="smaj:SPT_WORK_ORDER=1 pmaj:SPT_WORK_ORDER=2"
 echo "== config 1 wavefront" >> gpurun_out/ab.log
 VARIANTS="smaj= pmaj=" ENVS="$E" ROUNDS=3 bash tools/ab.sh > /dev/null || exit $?
 echo "== config 1 fused" >> gpurun_out/ab.log
