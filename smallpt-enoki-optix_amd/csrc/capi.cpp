@@ -1544,7 +1544,8 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         // fork: the sub-wavefront streams start after everything queued so far
         HIP_TRY(hipEventRecord(ws.fork_ev, stream));
         for (int k = 1; k < K; k++) HIP_TRY(hipStreamWaitEvent(strm[k], ws.fork_ev, 0));
-        uint64_t started[kMaxStreams], sub_end[kMaxStreams];  // work items known started; end of the share
+        uint64_t started[kMaxStreams], sub_begin[kMaxStreams], sub_end[kMaxStreams];  // work items known
+                                                                                      // started; the share
         for (int k = 0; k < K; k++) {
             Sub& b = ws.sub[k];
             // contiguous share of the chunk's work items (sample-major); pixel-major
@@ -1567,6 +1568,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             ra[k].surv_clear = nullptr;
             ra[k].casts_in = nullptr;
             const uint32_t first = (uint32_t)std::min<uint64_t>(b.cap, we - wb);
+            sub_begin[k] = wb;
             sub_end[k] = we;
             started[k] = wb + first;
             if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], first, strm[k]); }))) return st;
@@ -1585,7 +1587,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         uint64_t pend_it[kMaxStreams], limit[kMaxStreams];
         bool live[kMaxStreams];
         for (int k = 0; k < K; k++) {
-            known[k] = (uint32_t)std::min<uint64_t>(ws.sub[k].cap, started[k] - (w0 + L * k / K));
+            known[k] = (uint32_t)std::min<uint64_t>(ws.sub[k].cap, started[k] - sub_begin[k]);
             cur[k] = 0;
             pending[k] = -1;
             pend_cur[k] = 0;

@@ -299,6 +299,27 @@ def test_work_order_bitexact(small, pipeline, block, order, per_chunk):
     np.testing.assert_array_equal(got_u, ref_u)
 
 
+@pytest.mark.parametrize("order", [1, 2])
+def test_work_order_stream_shares(small, order):
+    """Pixel-major work splits a chunk's samples over the streams (21 samples:
+    5 / 5 / 5 / 6), so a stream's share no longer starts at k/K of the chunk's
+    work items; the first isect / shade grids must cover the stream's whole
+    first refill (a grid sized from k/K once dropped paths)."""
+    m, albedo, osc = small
+    w, h, spp, depth = 64, 48, 21, 3
+    cfg = sptamd.default_config()
+    cfg.work_order = order
+    cfg.streams = 4
+    s = sptamd.Scene(config=cfg)
+    s.add_arrays(m)
+    s.commit(0)
+    s.backend.set_albedo(albedo)
+    got, st = render(s, w, h, spp, depth, pipeline="wavefront", wavefront_paths=8000, rr_start_depth=2)
+    ref, casts = osc.render(O.reference_params(w, h, spp, depth, rr_start_depth=2))
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+
+
 def test_config_through_the_abi(small, monkeypatch):
     """Knobs set through spt_config (no environment variable anywhere) change
     scheduling only; invalid values are rejected by spt_scene_set_config."""
