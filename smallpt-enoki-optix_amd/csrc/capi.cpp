@@ -1355,13 +1355,17 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     bool fused = cfg.pipeline == SPT_PIPELINE_AUTO ? P * p.spp <= fused_max : cfg.pipeline == SPT_PIPELINE_FUSED;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
     if ((p.flags & SPT_FLAG_WAVEFRONT) || trav_stats) fused = false;
-    // Work order (spt_config.work_order).  AUTO: pixel-major once the scene
-    // outgrows an XCD's L2 — the paths in flight then cover a band of the
-    // tile, whose scene working set is smaller (config 3 +26 %, fused config
-    // 1 +7 %, config 4 +3 %, wavefront config 1 +0.4 %); a scene that fits has
-    // nothing to gain (config 2 -4.6 %; profiles/r02_workorder).
-    const uint32_t pixel_major = cfg.work_order == SPT_WORK_PIXEL_MAJOR ||
-                                 (cfg.work_order == SPT_WORK_AUTO && sc->stats.device_bytes >= kPixelMajorMinSceneBytes);
+    // Work order (spt_config.work_order).  AUTO, measured (DESIGN.md §4,
+    // profiles/r02_workorder): pixel-major for a scene larger than the
+    // Infinity Cache (config 4: +3.8 %; the paths in flight then cover a band
+    // of the tile, whose scene working set is smaller), and in the fused
+    // kernel for tiles of >= 16M paths (config 1 tiles of N = 1 / 2 / 4:
+    // +6.7 / +3.9 / +2.1 %, N = 8: -2.7 %); sample-major otherwise (wavefront
+    // config 1 neutral, config 3 -2.8 %, config 2 -4.6 %).
+    const uint32_t pixel_major =
+        cfg.work_order == SPT_WORK_PIXEL_MAJOR ||
+        (cfg.work_order == SPT_WORK_AUTO && (sc->stats.device_bytes >= kPixelMajorMinSceneBytes ||
+                                             (fused && P * p.spp >= kPixelMajorMinFusedPaths)));
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);

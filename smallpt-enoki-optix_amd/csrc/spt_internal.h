@@ -23,7 +23,10 @@ constexpr uint32_t kShadeBlock = SPT_SHADE_BLOCK;  // shade: 8 waves, one queue 
 constexpr uint32_t kMetaDepthBits = 8;      // meta = sample << 8 | depth
 constexpr uint32_t kIsectChunk = 128;       // dynamic-share queue indices a wave takes per atomic
 constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lanes are idle
-constexpr uint64_t kPixelMajorMinSceneBytes = 4ull << 20;  // SPT_WORK_AUTO: pixel-major from one XCD's L2 up
+// SPT_WORK_AUTO: pixel-major for scenes beyond the Infinity Cache, and in the
+// fused kernel for tiles of at least 16M paths (capi.cpp spt_render)
+constexpr uint64_t kPixelMajorMinSceneBytes = 256ull << 20;
+constexpr uint64_t kPixelMajorMinFusedPaths = 16ull << 20;
 
 // Path modes: what a path carries besides its ray.  The scene decides
 // (spt_render): unit = every albedo 1 and no emitters, the reference's own
