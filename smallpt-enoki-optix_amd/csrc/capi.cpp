@@ -1517,8 +1517,6 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.P = (uint32_t)P; F.W = p.width; F.max_depth = p.max_depth;
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
         F.tile_index = p.tile_index; F.tile_count = p.tile_count; F.rows_per_group = p.rows_per_group;
-        F.pixel_block = cfg.pixel_block;
-        F.work_order = pixel_major;
         F.refill_idle = cfg.fused_refill_idle;
         // a small static share: the fused lanes' path lengths vary far more
         // than one cast's, so most work is taken dynamically (1/8 tile of
@@ -1533,7 +1531,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             F.work0 = (uint64_t)s0 * P;
             F.count = (uint32_t)((uint64_t)ns * P);  // <= 4 GiB / 12 B per chunk
             F.sample0 = s0;
-            F.chunk_ns = ns;
+            F.pm_ns = pixel_major ? ns : 0;
             HIP_TRY(hipMemsetAsync(F.next, 0, sizeof(uint32_t), stream));
             if ((st = mark(1, stream, [&] { return launch_fused(F, mode, stream, &lanes); }))) return st;
             if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;

@@ -877,7 +877,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     }
     if (i >= total) return;
     uint32_t s, q, lx, ly;
-    work_item(cur + i, a.chunk_s0, a.chunk_ns, a.P, a.work_order, s, q);
+    work_item((uint32_t)(cur + i - (uint64_t)a.chunk_s0 * a.P), a.chunk_s0, a.chunk_ns, a.P, a.work_order != 0, s, q);
     work_pixel(q, a.W, a.P, a.pixel_block, lx, ly);
     const uint32_t p = ly * a.W + lx;
     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
@@ -1192,10 +1192,10 @@ void render_fused_kernel(FusedArgs a) {
                 }
                 if (term) {
                     if (kMode == kModeUnit) {
-                        a.sflag[film_slot(sample - a.sample0, pix, a.P, a.chunk_ns, a.work_order)] = slot == -1 ? 1 : 0;
+                        a.sflag[film_slot(sample - a.sample0, pix, a.P, a.pm_ns, a.pm_ns != 0)] = slot == -1 ? 1 : 0;
                     } else {
                         size_t cs;
-                        float* f = film_rgb(a.sfilm, sample - a.sample0, pix, a.P, a.chunk_ns, a.work_order, cs);
+                        float* f = film_rgb(a.sfilm, sample - a.sample0, pix, a.P, a.pm_ns, a.pm_ns != 0, cs);
                         f[0] = lr;
                         f[cs] = lg;
                         f[2 * cs] = lb;
@@ -1217,10 +1217,8 @@ void render_fused_kernel(FusedArgs a) {
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
                 if (!busy && !pending && rank < take) {
-                    uint32_t q, lx, ly;
-                    work_item(a.work0 + pool + rank, a.sample0, a.chunk_ns, a.P, a.work_order, sample, q);
-                    work_pixel(q, a.W, a.P, a.pixel_block, lx, ly);
-                    pix = ly * a.W + lx;
+                    work_item(pool + rank, a.sample0, a.pm_ns, a.P, a.pm_ns != 0, sample, pix);  // work0 = sample0 * P
+                    const uint32_t lx = pix % a.W, ly = pix / a.W;  // scanline (pixel blocks: refill_kernel only)
                     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
                     gpix = gy * a.W + lx;                          // main.cpp:379-382
                     Pcg32 rng;

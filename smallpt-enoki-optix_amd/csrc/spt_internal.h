@@ -292,8 +292,8 @@ struct FusedArgs {
     uint64_t work0, initstate;
     uint32_t count, P, W, sample0, max_depth, rr_start, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
-    uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
-    uint32_t work_order, chunk_ns;  // 1: pixel-major work items (chunk of chunk_ns samples)
+    uint32_t pm_ns;             // pixel-major work items: the chunk's sample count (0: sample-major);
+                                // one argument for both, the kernel is short of SGPRs
     uint32_t refill_idle, static_share_q8, chunk, grid_q8;
     float env_r, env_g, env_b;
 };
@@ -324,21 +324,18 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
 // pixels of one row (B = 8), and bounce rays inherit that locality through
 // the order-preserving compaction.  Any B covers every pixel once, so the
 // image does not depend on it.  B <= 1: scanline order.
-// Work item w of the chunk of samples [s0, s0 + ns) -> (sample, pixel-order
-// index q).  Sample-major (order 0): w = s * P + q, so the paths in flight
-// cover a few samples of the whole tile.  Pixel-major (order 1): a pixel's ns
-// samples are consecutive work items, so a wave starts 64 samples of one
-// pixel and a contiguous share of the queue covers a band of the tile.  Both
-// cover every (sample, pixel) of the chunk once.
-SPT_HD void work_item(uint64_t w, uint32_t s0, uint32_t ns, uint32_t P, uint32_t order, uint32_t& s, uint32_t& q) {
-    if (order == 0) {
-        s = (uint32_t)(w / P);
-        q = (uint32_t)(w - (uint64_t)s * P);
-        return;
-    }
-    const uint32_t local = (uint32_t)(w - (uint64_t)s0 * P);
-    q = local / ns;
-    s = s0 + (local - q * ns);
+// Work item `local` (counted from the chunk's start) of the chunk of samples
+// [s0, s0 + ns) -> (sample, pixel-order index q).  Sample-major (pm false):
+// local = (s - s0) * P + q, so the paths in flight cover a few samples of the
+// whole tile.  Pixel-major: a pixel's ns samples are consecutive work items,
+// so a wave starts 64 samples of one pixel and a contiguous share of the queue
+// covers a band of the tile.  One 32-bit division by d = pm ? ns : P serves
+// both.  Both cover every (sample, pixel) of the chunk once.
+SPT_HD void work_item(uint32_t local, uint32_t s0, uint32_t ns, uint32_t P, bool pm, uint32_t& s, uint32_t& q) {
+    const uint32_t d = pm ? ns : P;
+    const uint32_t a = local / d, b = local - a * d;
+    s = s0 + (pm ? b : a);
+    q = pm ? a : b;
 }
 
 // Per-(sample, pixel) film slot of a chunk of ns samples: [sample][pixel] for
