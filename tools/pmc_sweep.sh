@@ -14,7 +14,7 @@ csvs=""
 for ctrs in "$@"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex ${KERNEL:-isect_queue} -d "$out/p$i" -o run --output-format csv \
-      -- python bench.py --config ${CONFIG:-1} --steps 1 --warmup 1 --no-cpu-baseline > "$out/p$i.log" 2>&1
+      -- python bench.py --config ${CONFIG:-1} --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$out/p$i.log" 2>&1
   rc=$?
   echo "== pass $i ($ctrs) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$i.log"; exit $rc; fi
