@@ -312,6 +312,7 @@ def main():
         wo = scene.backend.config["work_order"]
         work_order = {1: "sample-major", 2: "pixel-major"}.get(wo) or (
             ("pixel-major" if sstats["device_bytes"] >= 256 << 20 or (fused and W * H * args.spp // world >= 16 << 20)
+             or (not fused and sstats["device_bytes"] >= 4 << 20 and W * H // world <= 4 << 20)
              else "sample-major") + " (auto)")
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
@@ -361,8 +362,9 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
-            "work_order_rule": "auto: pixel-major for scenes of >= 256 MiB on the device and for fused tiles of "
-                               ">= 16M paths, else sample-major (DESIGN.md §4)",
+            "work_order_rule": "auto: pixel-major for scenes of >= 256 MiB, fused tiles of >= 16M paths and "
+                               "wavefront tiles of <= 4M px over scenes of >= 4 MiB (24M paths in flight), "
+                               "else sample-major (DESIGN.md §4)",
             "pipeline_rule": "auto: fused for tiles of <= 32M paths, else wavefront (DESIGN.md §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),

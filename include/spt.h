@@ -233,9 +233,11 @@ typedef struct spt_config {
     uint32_t work_order;            /* SPT_WORK_*: the order paths start in — sample-major (every
                                        pixel of a sample, then the next sample) or pixel-major (a
                                        pixel's samples together); AUTO: pixel-major for scenes of
-                                       >= 256 MiB on the device and for fused tiles of >= 16M
-                                       paths; the image does not depend on
-                                       it                                                [0..2] */
+                                       >= 256 MiB on the device, for fused tiles of >= 16M
+                                       paths, and for wavefront tiles of <= 4M pixels over
+                                       scenes of >= 4 MiB (then 24M paths in flight if
+                                       wavefront_paths is left at 32M); the
+                                       image does not depend on it                       [0..2] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

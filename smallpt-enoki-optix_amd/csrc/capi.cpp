@@ -692,7 +692,7 @@ void spt_default_config(spt_config* c) {
     c->stack_slack = 0;
     c->pipeline = SPT_PIPELINE_AUTO;
     c->fused_max_paths = 1ull << 25;
-    c->wavefront_paths = 1u << 25;
+    c->wavefront_paths = kDefaultWavefrontPaths;
     c->streams = 4;
     c->isect_refill_idle = 24;
     c->isect_static_share_q8 = 128;
@@ -1358,14 +1358,20 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     // Work order (spt_config.work_order).  AUTO, measured (DESIGN.md §4,
     // profiles/r02_workorder): pixel-major for a scene larger than the
     // Infinity Cache (config 4: +3.8 %; the paths in flight then cover a band
-    // of the tile, whose scene working set is smaller), and in the fused
-    // kernel for tiles of >= 16M paths (config 1 tiles of N = 1 / 2 / 4:
-    // +6.7 / +3.9 / +2.1 %, N = 8: -2.7 %); sample-major otherwise (wavefront
-    // config 1 neutral, config 3 -2.8 %, config 2 -4.6 %).
+    // of the tile, whose scene working set is smaller); in the fused kernel
+    // for tiles of >= 16M paths (config 1 tiles of N = 1 / 2 / 4: +6 / +3 /
+    // +2.8 %, N = 8: -1.5 %); in the wavefront for a scene that outgrows an
+    // XCD's L2 on a tile of <= 4M pixels, with 24M paths in flight unless
+    // set (config 1 +5.5 %); sample-major otherwise (config 3's 16.7M-pixel
+    // tile -2.1 %, smallpt's cache-resident scene -4.6 %).
+    const uint64_t scene_bytes = sc->stats.device_bytes;
+    const bool wave_pm = !fused && scene_bytes >= kPixelMajorMinWaveSceneBytes && P <= kPixelMajorMaxWaveTilePx;
     const uint32_t pixel_major =
         cfg.work_order == SPT_WORK_PIXEL_MAJOR ||
-        (cfg.work_order == SPT_WORK_AUTO && (sc->stats.device_bytes >= kPixelMajorMinSceneBytes ||
-                                             (fused && P * p.spp >= kPixelMajorMinFusedPaths)));
+        (cfg.work_order == SPT_WORK_AUTO && (scene_bytes >= kPixelMajorMinSceneBytes ||
+                                             (fused && P * p.spp >= kPixelMajorMinFusedPaths) || wave_pm));
+    if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
+        C = kPixelMajorWavefrontPaths;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);

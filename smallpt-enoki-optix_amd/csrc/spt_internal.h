@@ -27,6 +27,13 @@ constexpr uint32_t kRefillIdle = 16;        // refill a wave once this many lane
 // fused kernel for tiles of at least 16M paths (capi.cpp spt_render)
 constexpr uint64_t kPixelMajorMinSceneBytes = 256ull << 20;
 constexpr uint64_t kPixelMajorMinFusedPaths = 16ull << 20;
+// ... and in the wavefront for scenes beyond one XCD's L2 on tiles of <= 4M
+// pixels, with 24M paths in flight when the in-flight count is left at its
+// default (32M)
+constexpr uint64_t kPixelMajorMinWaveSceneBytes = 4ull << 20;
+constexpr uint64_t kPixelMajorMaxWaveTilePx = 4ull << 20;
+constexpr uint32_t kDefaultWavefrontPaths = 1u << 25;
+constexpr uint64_t kPixelMajorWavefrontPaths = 24ull << 20;
 
 // Path modes: what a path carries besides its ray.  The scene decides
 // (spt_render): unit = every albedo 1 and no emitters, the reference's own
