@@ -155,7 +155,8 @@ def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
 def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     """Oracle (oracle/, a C restatement of main.cpp:354-446, binned-SAH BVH2,
     one pthread per CPU this process may use) on a bounded row sample of the
-    same workload, on this host's cores."""
+    same workload, on this host's cores.  Returns the record and the oracle's
+    (rows, film) so the caller can check the GPU image against it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
@@ -172,12 +173,16 @@ def cpu_baseline(mesh, args, threads, kw, albedo, emission):
     dt = time.perf_counter() - t0
     # scale the sample to ~cpu_baseline_seconds of work, rows spread over the image
     want = int(max(1, min(args.height, len(rows) * args.cpu_baseline_seconds / max(dt, 1e-3))))
+    # the whole image when that costs at most ~3x the budget: the GPU image is
+    # then checked against the oracle row for row (the "parity" field)
+    if args.height * dt / len(rows) <= 3.0 * args.cpu_baseline_seconds:
+        want = args.height
     rows = np.unique(np.linspace(0, args.height - 1, want).astype(np.int32))
     t0 = time.perf_counter()
-    _, casts = sc.render(p, rows=rows, nthreads=threads)
+    film, casts = sc.render(p, rows=rows, nthreads=threads)
     dt = time.perf_counter() - t0
     paths = rows.size * args.width * args.spp
-    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+    return (rows, film), {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "cpu": _cpu_model(), "cpus": share_src,
             "sample": f"{rows.size} of {args.height} rows (evenly spaced) x {args.width} px x {args.spp} spp, "
                       f"depth {args.depth}: {paths} paths, {casts} casts in {dt:.2f} s "
@@ -191,7 +196,7 @@ def main():
     import torch.distributed as dist
 
     import sptamd
-    from sptamd import scenes
+    from sptamd import _lib, scenes
     from sptamd.distributed import TileGather
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -252,50 +257,85 @@ def main():
 
     gather_ev = []
 
-    def step(timed=False):
-        _, st = scene.render(params, film=film, stream=stream)
+    def check_work(st):
+        """Device-counted work of one render against the job (main.cpp:385-429
+        renders every pixel x sample): paths started == paths ended == tile
+        pixels x spp, and no per-sample film slot left unwritten."""
+        want = st["tile_rows"] * W * args.spp
+        bad = (st["paths_started"] != want or st["paths_terminated"] != want or st["film_slots_unwritten"] != 0)
+        if bad:
+            raise RuntimeError(f"rank {rank}: lost work: started {st['paths_started']}, terminated "
+                               f"{st['paths_terminated']}, unwritten film slots {st['film_slots_unwritten']}, "
+                               f"expected {want} paths")
+        return want
+
+    def step(p, timed=False, evs=None):
+        _, st = scene.render(p, film=film, stream=stream)
         if timed:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
         tg.gather()
         if timed:
             e1.record(stream)
-            gather_ev.append((e0, e1))
+            evs.append((e0, e1))
         return st
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
-           "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0}
-    st = {}
-    for _ in range(args.steps):
-        st = step(timed=True)
-        for k in agg:
-            agg[k] += st[k]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([agg["ray_casts"], agg["isect_ms"], agg["iterations"], agg["continuations"]],
-                           dtype=torch.float64, device=rdev)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        agg_casts_all = float(tot[0].item())
-        agg_cont_all = float(tot[3].item())
-    else:
-        agg_casts_all = float(agg["ray_casts"])
-        agg_cont_all = float(agg["continuations"])
+    def timed_loop(p, evs):
+        """W untimed steps, then exactly K timed steps between barriers +
+        synchronize; returns (max-over-ranks seconds, summed stats, last stats,
+        device-counted paths of all ranks)."""
+        for _ in range(args.warmup):
+            check_work(step(p))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
+               "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0,
+               "paths": 0}
+        sts = []
+        for _ in range(args.steps):
+            st = step(p, timed=True, evs=evs)
+            sts.append(st)
+            for k in agg:
+                agg[k] += st[k]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        for st in sts:  # after the timed region: the counters were read back by every render anyway
+            check_work(st)
+        tot = [agg["ray_casts"], agg["continuations"], agg["paths"]]
+        if world > 1:
+            rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+            t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            tt = torch.tensor(tot, dtype=torch.float64, device=rdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.SUM)
+            tot = [float(x) for x in tt.tolist()]
+        return elapsed, agg, sts[-1], tot
 
-    paths = W * H * args.spp * args.steps
+    elapsed, agg, st, (agg_casts_all, agg_cont_all, paths) = timed_loop(params, gather_ev)
+    if paths != W * H * args.spp * args.steps:
+        raise RuntimeError(f"device-counted paths {paths} != {W * H * args.spp * args.steps} (W x H x spp x steps)")
+    image_main = tg.image.clone() if rank == 0 else None
+    # At N > 1 the library's job-size rule runs the fused kernel on each rank's
+    # tile; the north-star wavefront pipeline is timed beside it on the same
+    # tiles (a second loop after the first), so the N-GPU line says what both do.
+    wave_leg = None
+    if world > 1 and st.get("fused") and args.pipeline == "auto":
+        pw = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
+                                wavefront_paths=args.wavefront, timing=True, pipeline="wavefront", **kw)
+        w_el, w_agg, w_st, w_tot = timed_loop(pw, [])
+        w_paths = w_tot[2]
+        wave_leg = {"pipeline": "wavefront", "value": round(w_paths / w_el / 1e6, 3),
+                    "ms_per_step": round(w_el / args.steps * 1e3, 3), "streams": w_st.get("streams"),
+                    "isect_busy_ms_per_step_rank0": round(w_agg["isect_busy_ms"] / args.steps, 4),
+                    "paths_device_counted": int(w_paths)}
+        if rank == 0 and image_main is not None:
+            wave_leg["image_equal_to_fused"] = bool(torch.equal(image_main, tg.image))
     value = paths / elapsed / 1e6
     gather_ms = sum(e0.elapsed_time(e1) for e0, e1 in gather_ev) / max(1, len(gather_ev))
     if rank == 0:
@@ -306,20 +346,23 @@ def main():
         # intervals (HIP events on each launch's own stream): the time the
         # kernel occupies the chip, <= ms_per_step.  `per_launch` keeps the
         # per-launch figure (a 1/K-chip rate when K > 1).  Fused:
-        # render_fused_kernel, whose only HBM stream is the per-sample film
-        # write (12 B per path; rays stay in registers).
+        # render_fused_kernel runs the whole path (trace + shade + bounce) in
+        # registers, so its unit is the path and its bytes are SURVEY §8(d)'s
+        # whole-path model B_path = 84 + 120 S + 60 C (what the wavefront moves
+        # for the same path) over the fused launches' busy time.
         fused = bool(st.get("fused"))
-        wo = scene.backend.config["work_order"]
-        work_order = {1: "sample-major", 2: "pixel-major"}.get(wo) or (
-            ("pixel-major" if sstats["device_bytes"] >= 256 << 20 or (fused and W * H * args.spp // world >= 16 << 20)
-             or (not fused and sstats["device_bytes"] >= 4 << 20 and W * H // world <= 4 << 20)
-             else "sample-major") + " (auto)")
+        work_order = {1: "sample-major", 2: "pixel-major"}.get(st.get("work_order"), "?")
+        if scene.backend.config["work_order"] == 0:
+            work_order += " (auto)"
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
         casts_per_launch = agg["ray_casts"] / launches
+        s_bar = agg_casts_all / paths
+        c_bar = agg_cont_all / paths
+        b_path = 84.0 + 120.0 * s_bar + 60.0 * c_bar
         if fused:
-            bytes_per_unit, kernel_bytes_per_unit = FUSED_BYTES_PER_PATH, FUSED_BYTES_PER_PATH
-            total_bytes = st["paths"] * args.steps * FUSED_BYTES_PER_PATH
+            bytes_per_unit = kernel_bytes_per_unit = round(b_path, 2)
+            total_bytes = agg["paths"] * b_path  # rank 0's paths over rank 0's busy time
         else:
             bytes_per_unit, kernel_bytes_per_unit = ISECT_BYTES_PER_CAST, KERNEL_BYTES_PER_CAST
             total_bytes = agg["ray_casts"] * ISECT_BYTES_PER_CAST
@@ -327,26 +370,30 @@ def main():
         busy_ms = agg["isect_busy_ms"]
         achieved = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
         per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        # whole-path bytes: B_path = 84 + 120 S + 60 C, S = casts and
-        # C = continuations per path, over the whole frame time, against the spec
-        # peak and a stream-copy peak measured here (BASELINE.md plan)
-        s_bar = agg_casts_all / paths
-        c_bar = agg_cont_all / paths
-        b_path = 84.0 + 120.0 * s_bar + 60.0 * c_bar
+        # whole-path bytes over the whole frame time, against the
+        # spec peak and a stream-copy peak measured here (BASELINE.md plan)
         path_gbs = b_path * paths / elapsed / 1e9
         copy_gbs = stream_copy_gbs(torch, dev)
-        pmc = None
-        if os.path.exists(PMC_JSON) and not fused and world == 1:  # PMC passes (profiles/, tools/pmc_isect.py)
-            pmc = json.load(open(PMC_JSON)).get(f"config{args.config}")
-        traffic = traffic_per_cast = None
-        if pmc and pmc.get("traffic_bytes_per_cast"):
-            traffic_per_cast = pmc["traffic_bytes_per_cast"]
-            traffic = round(traffic_per_cast * casts_per_launch)
+        build_id = _lib.lib.spt_build_id().decode()
+        pmc = pmc_note = None
+        key = f"config{args.config}" + ("_fused" if fused else "")
+        if os.path.exists(PMC_JSON) and world == 1:  # PMC passes (profiles/, tools/pmc_isect.sh)
+            pmc = json.load(open(PMC_JSON)).get(key)
+            if pmc and pmc.get("build_id") != build_id:
+                pmc_note = (f"{key} was measured on build {pmc.get('build_id')}, this library is {build_id}: "
+                            "not used")
+                pmc = None
+        unit_name = "path" if fused else "cast"
+        traffic = traffic_per_unit = None
+        if pmc and pmc.get(f"traffic_bytes_per_{unit_name}"):
+            traffic_per_unit = pmc[f"traffic_bytes_per_{unit_name}"]
+            traffic = round(traffic_per_unit * (agg["paths"] / launches if fused else casts_per_launch))
         valu = None
-        if pmc and pmc.get("valu_insts_per_cast") and busy_ms > 0:
-            rate = pmc["valu_insts_per_cast"] * agg["ray_casts"] / (busy_ms * 1e-3) / 1e9
-            valu = {"insts_per_cast": round(pmc["valu_insts_per_cast"], 2), "achieved": round(rate, 1),
-                    "peak": VALU_PEAK_G, "unit": "G wave64 VALU instr/s over isect busy time",
+        if pmc and pmc.get(f"valu_insts_per_{unit_name}") and busy_ms > 0:
+            units = agg["paths"] if fused else agg["ray_casts"]
+            rate = pmc[f"valu_insts_per_{unit_name}"] * units / (busy_ms * 1e-3) / 1e9
+            valu = {f"insts_per_{unit_name}": round(pmc[f"valu_insts_per_{unit_name}"], 2), "achieved": round(rate, 1),
+                    "peak": VALU_PEAK_G, "unit": "G wave64 VALU instr/s over kernel busy time",
                     "frac": round(rate / VALU_PEAK_G, 4)}
         rec = {
             "metric": "Mpaths/sec (pixels x spp / s), mitsuba.obj-standin 1024^2 x 64spp, depth 8"
@@ -362,6 +409,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic ({args.scene} stand-in generated in-run; reference asset absent)",
+            "work_check": {"paths_device_counted": int(paths), "expected": W * H * args.spp * args.steps,
+                           "rule": "every step, every rank: paths started == paths ended == tile px x spp, "
+                                   "0 film slots unwritten (spt_render_stats)"},
+            "dist": {"backend": dist.get_backend() if world > 1 else None, "world_size": world},
             "work_order_rule": "auto: pixel-major for scenes of >= 256 MiB, fused tiles of >= 16M paths and "
                                "wavefront tiles of <= 4M px over scenes of >= 4 MiB (24M paths in flight), "
                                "else sample-major (DESIGN.md §4)",
@@ -372,16 +423,18 @@ def main():
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
-                       "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(agg_casts_all / paths, 4),
+                       "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(s_bar, 4),
                        "work_order": work_order},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",
-                         "basis": "algorithmic bytes of all launches / union of their intervals (isect busy)",
+                         "basis": ("SURVEY 8(d) whole-path bytes of rank 0's paths / union of its fused launch "
+                                   "intervals") if fused else
+                                  "algorithmic bytes of all launches / union of their intervals (isect busy)",
                          "bytes_per_unit": bytes_per_unit, "kernel_bytes_per_unit": kernel_bytes_per_unit,
                          "unit_of_work": "path" if fused else "ray cast",
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                         "traffic_per_unit": traffic_per_cast,
+                         "traffic_per_unit": traffic_per_unit,
                          "traffic_ratio": round(traffic / bytes_per_launch, 3) if traffic else None,
                          "busy_ms_per_step": round(busy_ms / args.steps, 4),
                          "launches_per_step": round(launches / args.steps, 2),
@@ -389,7 +442,9 @@ def main():
                          "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None,
                          "per_launch": {"achieved": round(per_launch, 2), "frac": round(per_launch / HBM_PEAK_GBS, 5),
                                         "note": f"per-launch duration; {st.get('streams')} streams overlap"},
-                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) + f"#config{args.config}" if pmc else None,
+                         "pmc_source": os.path.relpath(PMC_JSON, ROOT) + "#" + key if pmc else None,
+                         "pmc_note": pmc_note,
+                         "build_id": build_id,
                          "valu": valu,
                          "stream_copy_peak": round(copy_gbs, 1),
                          "path": {"bytes_per_path": round(b_path, 1),
@@ -403,10 +458,18 @@ def main():
             "bvh": dict({k: sstats[k] for k in ("builder", "nodes", "max_depth", "build_ms", "sah_cost", "device_bytes")},
                         commit_s=round(t_commit, 3)),
         }
+        if wave_leg:
+            rec["wavefront_leg"] = wave_leg
         if args.save:
-            np.save(args.save, tg.image.cpu().numpy())
+            np.save(args.save, image_main.cpu().numpy())
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads, kw, alb, emi)
+            (orows, ofilm), rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads, kw, alb, emi)
+            got = image_main[:, torch.as_tensor(orows, dtype=torch.long, device=dev), :].cpu().numpy()
+            diff = got != ofilm
+            rec["parity"] = {"rows": int(orows.size), "of_rows": H, "bitexact": bool(not diff.any()),
+                             "values_differing": int(diff.sum()),
+                             "max_abs_diff": float(np.abs(got - ofilm).max()) if got.size else 0.0,
+                             "against": "oracle/ (C restatement of main.cpp:354-446), the cpu_baseline render"}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

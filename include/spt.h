@@ -104,7 +104,8 @@ typedef struct spt_render_params {
 } spt_render_params;
 
 typedef struct spt_render_stats {
-    uint64_t paths;             /* pixels x spp rendered by this call */
+    uint64_t paths;             /* paths rendered by this call, counted on the device (= paths_terminated);
+                                   a complete render has paths == tile pixels x spp */
     uint64_t ray_casts;         /* closest/any-hit queries traced */
     uint64_t continuations;     /* paths that bounced into a next cast */
     uint64_t regenerations;     /* camera rays started by refills after the first launch */
@@ -123,6 +124,17 @@ typedef struct spt_render_stats {
     double isect_busy_ms;       /* SPT_FLAG_TIMING: union of the isect launch intervals
                                    (launches on the K streams overlap; isect_ms sums them) */
     uint64_t isect_max_stack;   /* SPT_FLAG_TRAVERSAL_STATS: deepest LDS stack entry used */
+    /* Work accounting, counted on the device (not derived from the params):
+     * every (sample, pixel) of the tile is one path; a complete render has
+     * paths_started == paths_terminated == tile pixels x spp and
+     * film_slots_unwritten == 0, which together mean every path's film slot
+     * was written exactly once (main.cpp:385-429 renders every pixel x sample). */
+    uint64_t paths_started;     /* camera rays generated (refill launches / fused kernel) */
+    uint64_t paths_terminated;  /* paths that ended: casts - continuations, from the queue counts */
+    uint64_t film_slots_unwritten; /* per-(sample, pixel) film slots still holding the pre-render
+                                      sentinel when the resolve read them */
+    uint32_t work_order;        /* the order that ran: SPT_WORK_SAMPLE_MAJOR or SPT_WORK_PIXEL_MAJOR */
+    uint32_t reserved0;
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -335,8 +347,16 @@ spt_status spt_scene_cache_info(const char* path, spt_scene_stats* stats, spt_co
 /* OptixBackend::intersect (optix_backend.h:422-460) → __raygen__rg
  * (wavefront_isect.cu:80-112): one lane per ray; mask_size == 1 broadcasts
  * mask[0]; masked lanes write nothing; a miss writes tri_id = -1 (t/u/v
- * untouched); do_closest = 0 is OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT.
- * All pointers are device pointers; n rays. */
+ * untouched).  do_closest = 0 is the reference's any-hit query
+ * (OPTIX_RAY_FLAG_TERMINATE_ON_FIRST_HIT): traversal stops at the first
+ * triangle (or sphere) accepted in [tmin, tmax].  Deviation, documented: the
+ * reference launches that query with the closest-hit program disabled
+ * (OPTIX_RAY_FLAG_DISABLE_CLOSESTHIT, wavefront_isect.cu:104-105), so on a hit
+ * its tri_id / t / u / v come from payload registers nothing wrote
+ * (uninitialised); only "tri_id != -1" is meaningful there.  This library
+ * writes the first accepted hit's real record (tri_id, t, u, v of that
+ * triangle, not necessarily the nearest), which satisfies every use the
+ * reference makes of the result.  All pointers are device pointers; n rays. */
 spt_status spt_intersect(spt_scene scene, const spt_rays* rays, const uint8_t* mask,
                          uint32_t mask_size, const spt_hits* hits, uint32_t n,
                          int32_t do_closest, void* stream);
@@ -354,7 +374,13 @@ spt_status spt_hit_info_compute(spt_scene scene, const spt_rays* rays, const spt
  * Threading: a scene owns one render workspace (path queues, film chunks,
  * events), so spt_render calls on one scene are serialised by a per-scene
  * mutex (a second thread waits); render concurrently from one scene per
- * thread / device.  spt_scene_set_config takes the same mutex. */
+ * thread / device.  spt_scene_set_config and the other scene setters
+ * (albedo, emission, textures, spheres, material kinds) take the same mutex;
+ * spt_intersect / spt_hit_info_compute take it only to snapshot the scene's
+ * device arrays and knobs before their (asynchronous) launch.  A setter that
+ * replaces device arrays frees the old ones, so it must not run while a
+ * launch that read them is still in flight on some stream: synchronise
+ * first. */
 spt_status spt_render(spt_scene scene, const spt_render_params* params, float* film_dev,
                       spt_render_stats* stats, void* stream);
 
@@ -368,6 +394,9 @@ void spt_default_params(spt_render_params* p);
 
 const char* spt_last_error(void);
 const char* spt_version(void);
+/* A hash of the sources and compiler flags this library was built from: profile
+ * data (profiles/isect_pmc.json) names the build it measured by this id. */
+const char* spt_build_id(void);
 
 /* ------------------------------------------------------------------ host */
 /* load_meshes (main.cpp:141-251): triangulating OBJ reader with tinyobj's

@@ -87,6 +87,7 @@ struct Counters {
 struct Stats {
     unsigned long long stats[3];  // casts, continuations, camera rays started
     unsigned long long trav[5];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps, max stack
+    unsigned long long unwritten; // film slots still holding the sentinel at resolve time
 };
 
 constexpr int kMaxStreams = 4;
@@ -436,6 +437,11 @@ extern "C" {
 
 const char* spt_last_error(void) { return g_last_error.c_str(); }
 const char* spt_version(void) { return "spt-mi355x 0.1 (gfx950 wavefront path tracer)"; }
+
+#ifndef SPT_BUILD_ID
+#define SPT_BUILD_ID "unknown"
+#endif
+const char* spt_build_id(void) { return SPT_BUILD_ID; }
 
 spt_status spt_init(int32_t device) {
     spt_status st = ensure_device();
@@ -1037,6 +1043,111 @@ spt_status cache_check_textures(const char* path, const char* what, const CacheH
     return SPT_OK;
 }
 
+// Content checks of a loaded BVH before it reaches the device (the checksums
+// only catch accidents): from the root, every reachable node index lies in the
+// node section and is reached once (a tree: traversal ends), the tree fits
+// the LDS stack the header declares, and every leaf's triangle slots lie in
+// [0, ntri).  Unreachable slots (holes between packed child groups) are not read.
+spt_status cache_check_nodes(const char* path, const char* what, const CacheHeader& h, const std::vector<uint8_t>& buf) {
+    const uint64_t nt = h.ntri;
+    if (nt == 0) return SPT_OK;
+    const uint64_t nslots = buf.size() / ((uint64_t)h.node_quads * 16);
+    const uint32_t* w = (const uint32_t*)buf.data();
+    const uint64_t stride = (uint64_t)h.node_quads * 4;  // words per node slot
+    std::vector<uint8_t> seen(nslots, 0);
+    std::vector<std::pair<uint64_t, uint32_t>> todo{{0, 1}};  // (node, level; root = 1)
+    seen[0] = 1;
+    uint32_t depth = 0;
+    const auto bad = [&](const char* why, uint64_t node) {
+        return fail(SPT_ERR_INVALID, "%s: %s: BVH node %llu: %s", what, path, (unsigned long long)node, why);
+    };
+    while (!todo.empty()) {
+        const uint64_t node = todo.back().first;
+        const uint32_t level = todo.back().second;
+        todo.pop_back();
+        depth = std::max(depth, level);
+        const uint32_t* n = w + node * stride;
+        auto child = [&](uint64_t c) -> bool {
+            if (c >= nslots || seen[c]) return false;
+            seen[c] = 1;
+            todo.push_back({c, level + 1});
+            return true;
+        };
+        if (h.stats.bvh_width == 2) {  // bvh_build.h: codes in word 12, 13
+            for (int k = 0; k < 2; k++) {
+                const int32_t code = (int32_t)n[12 + k];
+                if (code >= 0) {
+                    if (!child((uint64_t)code)) return bad("inner child out of range or reached twice", node);
+                } else {
+                    const uint32_t leaf = ~(uint32_t)code;
+                    if ((uint64_t)(leaf >> 3) + (leaf & 7u) + 1u > nt) return bad("leaf beyond the triangles", node);
+                }
+            }
+            continue;
+        }
+        // wide nodes: meta bytes, child-group word, triangle base (bvh_build.h)
+        uint8_t meta[8];
+        uint32_t nmeta, group, tri_base;
+        if (h.node6) {
+            std::memcpy(meta, &n[4], 4);
+            meta[4] = (uint8_t)n[5];
+            meta[5] = (uint8_t)(n[5] >> 8);
+            nmeta = 6;
+            group = n[6] & 0x00ffffffu;
+            tri_base = n[3];
+        } else {
+            std::memcpy(meta, &n[6], 8);
+            nmeta = 8;
+            group = n[4];
+            tri_base = n[5];
+        }
+        for (uint32_t c = 0; c < nmeta; c++) {
+            const uint32_t m = meta[c];
+            if (!m) continue;
+            if ((m & 0x18u) == 0x18u) {  // inner: 0b001_(24 + s)
+                const uint64_t cn = ((uint64_t)group << h.group_shift) + ((m & 31u) - 24u);
+                if (!child(cn)) return bad("inner child out of range or reached twice", node);
+            } else {  // leaf: unary(count) << 5 | offset
+                const uint32_t cnt = (uint32_t)__builtin_popcount(m >> 5);
+                if ((uint64_t)tri_base + (m & 31u) + cnt > nt) return bad("leaf beyond the triangles", node);
+            }
+        }
+    }
+    // the traversal stacks: BVH2 one entry per level below the root, a wide
+    // BVH depth - 1 entries (bvh8_stack_entries)
+    const uint32_t need = h.stats.bvh_width == 2 ? depth : (depth > 1 ? depth - 1 : 1);
+    if (need > h.stack_depth)
+        return fail(SPT_ERR_INVALID, "%s: %s: the BVH is %u levels deep, its stack holds %u entries", what, path, depth,
+                    h.stack_depth);
+    return SPT_OK;
+}
+
+// Index arrays of a loaded scene: orig2slot maps into the slots, every slot's
+// original id (v0.w) lies in [0, ntri), material kinds are SPT_MAT_*.
+spt_status cache_check_indices(const char* path, const char* what, const CacheHeader& h, uint32_t s,
+                               const std::vector<uint8_t>& buf) {
+    const uint64_t nt = h.ntri;
+    if (s == kSecOrig2Slot) {
+        const int32_t* o = (const int32_t*)buf.data();
+        for (uint64_t i = 0; i < nt; i++)
+            if (o[i] < 0 || (uint64_t)o[i] >= nt)
+                return fail(SPT_ERR_INVALID, "%s: %s: orig2slot[%llu] = %d outside [0, %llu)", what, path,
+                            (unsigned long long)i, o[i], (unsigned long long)nt);
+    } else if (s == kSecTris) {
+        const uint32_t* t = (const uint32_t*)buf.data();
+        for (uint64_t i = 0; i < nt; i++)
+            if (t[i * kTriQuads * 4 + 3] >= nt)
+                return fail(SPT_ERR_INVALID, "%s: %s: triangle slot %llu has id %u", what, path, (unsigned long long)i,
+                            t[i * kTriQuads * 4 + 3]);
+    } else if (s == kSecKinds) {
+        const uint32_t* k = (const uint32_t*)buf.data();
+        for (uint32_t i = 0; i < h.nkind; i++)
+            if (k[i] > SPT_MAT_GLASS)
+                return fail(SPT_ERR_INVALID, "%s: %s: material %u has kind %u", what, path, i, k[i]);
+    }
+    return SPT_OK;
+}
+
 }  // namespace
 
 spt_status spt_scene_save(spt_scene sc, const char* path, const void* extra, uint64_t extra_bytes) {
@@ -1187,6 +1298,8 @@ spt_status spt_scene_load(const char* path, spt_scene* out, void* extra, uint64_
     std::vector<uint8_t> buf;
     for (uint32_t s = 0; s < kNumSecs; s++) {
         if ((st = cache_read_section(f, path, what, h, s, buf))) return bail(st);
+        if ((st = s == kSecNodes ? cache_check_nodes(path, what, h, buf) : cache_check_indices(path, what, h, s, buf)))
+            return bail(st);
         switch (s) {
             case kSecNodes:
                 st = h.stats.bvh_width == 2 ? upload(&sc->nodes, buf.data(), buf.size())
@@ -1255,7 +1368,12 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     if (mask && mask_size != 1 && mask_size != n)
         return fail(SPT_ERR_INVALID, "spt_intersect: mask_size %u must be 1 or n=%u", mask_size, n);
     IsectPublicArgs a;
-    a.sc = sc->dev();
+    {  // a consistent snapshot of the device arrays and knobs (the scene setters change them under mu)
+        std::lock_guard<std::mutex> lock(sc->mu);
+        a.sc = sc->dev();
+        a.refill_idle = sc->cfg.public_refill_idle;
+        a.persistent = sc->cfg.public_persistent;
+    }
     a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
     a.dx = rays->dx; a.dy = rays->dy; a.dz = rays->dz;
     a.tmin = rays->tmin; a.tmax = rays->tmax;
@@ -1263,8 +1381,6 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
     a.n = n;
     a.closest = do_closest;
-    a.refill_idle = sc->cfg.public_refill_idle;
-    a.persistent = sc->cfg.public_persistent;
     HIP_TRY(launch_isect_public(a, (hipStream_t)stream));
     return SPT_OK;
 }
@@ -1275,15 +1391,21 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
     if (n == 0) return SPT_OK;
     if (!hits->tri_id || !hits->t || !hits->u || !hits->v)
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL hit plane");
-    // the rays are read only for the position (o + t d)
-    if ((out->px || out->py || out->pz) &&
-        (!rays->ox || !rays->oy || !rays->oz || !rays->dx || !rays->dy || !rays->dz))
+    // the rays are read for the position (o + t d), and on a scene with
+    // spheres for their normals too (the normal of a sphere hit is (p - c) / r)
+    const bool no_rays = !rays->ox || !rays->oy || !rays->oz || !rays->dx || !rays->dy || !rays->dz;
+    if ((out->px || out->py || out->pz) && no_rays)
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL ray plane (needed for the position)");
+    if (no_rays && sc->nsph > 0 && (out->gnx || out->gny || out->gnz || out->snx || out->sny || out->snz))
+        return fail(SPT_ERR_INVALID, "spt_hit_info_compute: NULL ray plane (a sphere hit's normal needs the hit point)");
     if (mask && mask_size != 1 && mask_size != n)
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: mask_size %u must be 1 or n=%u", mask_size, n);
     if (sc->ntri == 0 && sc->nsph == 0) return SPT_OK;
     HitInfoArgs a;
-    a.sc = sc->dev();
+    {
+        std::lock_guard<std::mutex> lock(sc->mu);
+        a.sc = sc->dev();
+    }
     a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
     a.dx = rays->dx; a.dy = rays->dy; a.dz = rays->dz;
     a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
@@ -1317,7 +1439,6 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const uint64_t P = (uint64_t)rows * p.width;
     spt_render_stats rs{};
     rs.tile_rows = rows;
-    rs.paths = P * p.spp;
     if (P == 0) {  // an empty tile: nothing to render, film untouched
         if (stats_out) *stats_out = rs;
         return SPT_OK;
@@ -1426,9 +1547,14 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const auto resolve = [&](uint32_t s0, uint32_t ns) {
         return mode == kModeUnit
                    ? launch_resolve_flags(sflag, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                          p.env[0], p.env[1], p.env[2], film_order, stream)
+                                          p.env[0], p.env[1], p.env[2], film_order, &ws.stats->unwritten, stream)
                    : launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                    film_order, stream);
+                                    film_order, &ws.stats->unwritten, stream);
+    };
+    // every slot of a chunk starts as the sentinel (kFlagSentinel / kFilmSentinel
+    // bytes), so the resolve counts slots no path wrote (spt_render_stats)
+    const auto clear_film = [&](uint32_t ns) {
+        return hipMemsetAsync(ws.film, 0xff, (size_t)ns * film_unit * P, stream);
     };
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
@@ -1538,6 +1664,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
             F.count = (uint32_t)((uint64_t)ns * P);  // <= 4 GiB / 12 B per chunk
             F.sample0 = s0;
             F.pm_ns = pixel_major ? ns : 0;
+            HIP_TRY(clear_film(ns));
             HIP_TRY(hipMemsetAsync(F.next, 0, sizeof(uint32_t), stream));
             if ((st = mark(1, stream, [&] { return launch_fused(F, mode, stream, &lanes); }))) return st;
             if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
@@ -1549,6 +1676,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     for (uint32_t s0 = 0; s0 < p.spp && !fused; s0 += chunk) {
         const uint32_t ns = std::min(chunk, p.spp - s0);
         const uint64_t w0 = (uint64_t)s0 * P, L = (uint64_t)ns * P;
+        HIP_TRY(clear_film(ns));
         // fork: the sub-wavefront streams start after everything queued so far
         HIP_TRY(hipEventRecord(ws.fork_ev, stream));
         for (int k = 1; k < K; k++) HIP_TRY(hipStreamWaitEvent(strm[k], ws.fork_ev, 0));
@@ -1686,7 +1814,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     }
     // pinned destination: a pageable one makes the copy a staged, slower transfer
     const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(ws.host_stats);
-    static_assert(sizeof(Stats) == 8 * sizeof(unsigned long long), "Stats is the 8 counters read back here");
+    static_assert(sizeof(Stats) == 9 * sizeof(unsigned long long), "Stats is the 9 counters read back here");
     HIP_TRY(hipMemcpyAsync(ws.host_stats, ws.stats, sizeof(Stats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
@@ -1698,6 +1826,11 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     rs.isect_lane_steps = hstats[5];
     rs.isect_wave_steps = hstats[6];
     rs.isect_max_stack = hstats[7];
+    rs.paths_started = hstats[2];
+    rs.paths_terminated = hstats[0] - hstats[1];  // every cast either continues or ends its path
+    rs.paths = rs.paths_terminated;
+    rs.film_slots_unwritten = hstats[8];
+    rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
     if (timing) {
         uint64_t nis = 0;
         std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin

@@ -1265,23 +1265,30 @@ void render_fused_kernel(FusedArgs a) {
 // Per-pixel sum of the per-sample contributions in sample order
 // (film += ... once per sample, main.cpp:407), then film /= spp (main.cpp:429).
 // Chunks of samples carry the running sum in acc.
+// Every slot of the chunk was set to kFilmSentinel before the render: a slot
+// still holding it was never written (a lost path), counted in *unwritten
+// (no atomic at all when every path wrote its slot).
 __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ sfilm, float* __restrict__ acc,
                                                       float* __restrict__ out, uint32_t P, uint32_t nsamples,
                                                       uint32_t first_chunk, uint32_t last_chunk, uint32_t spp,
-                                                      uint32_t order) {
+                                                      uint32_t order, unsigned long long* __restrict__ unwritten) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= P) return;
+    uint32_t lost = 0;
     for (uint32_t c = 0; c < 3; c++) {
         float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
         for (uint32_t s = 0; s < nsamples; s++) {
             size_t cs;
-            sum = sum + film_rgb(const_cast<float*>(sfilm), s, p, P, nsamples, order, cs)[c * cs];
+            const float x = film_rgb(const_cast<float*>(sfilm), s, p, P, nsamples, order, cs)[c * cs];
+            if (c == 0 && f2u(x) == kFilmSentinel) lost++;
+            sum = sum + x;
         }
         if (last_chunk)
             out[(size_t)c * P + p] = sum / (float)spp;
         else
             acc[(size_t)c * P + p] = sum;
     }
+    if (lost) atomicAdd(unwritten, (unsigned long long)lost);
 }
 
 // Unit mode: every escaped sample adds the sky radiance once, in sample order
@@ -1292,11 +1299,17 @@ __global__ __launch_bounds__(256) void resolve_flags_kernel(const uint8_t* __res
                                                             float* __restrict__ acc, float* __restrict__ out,
                                                             uint32_t P, uint32_t nsamples, uint32_t first_chunk,
                                                             uint32_t last_chunk, uint32_t spp, float env_r,
-                                                            float env_g, float env_b, uint32_t order) {
+                                                            float env_g, float env_b, uint32_t order,
+                                                            unsigned long long* __restrict__ unwritten) {
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= P) return;
-    uint32_t k = 0;
-    for (uint32_t s = 0; s < nsamples; s++) k += sflag[film_slot(s, p, P, nsamples, order)];
+    uint32_t k = 0, lost = 0;
+    for (uint32_t s = 0; s < nsamples; s++) {
+        const uint32_t f = sflag[film_slot(s, p, P, nsamples, order)];
+        lost += f == kFlagSentinel ? 1u : 0u;
+        k += f & 1u;
+    }
+    if (lost) atomicAdd(unwritten, (unsigned long long)lost);
     const float env[3] = {env_r, env_g, env_b};
     for (uint32_t c = 0; c < 3; c++) {
         float sum = first_chunk ? 0.0f : acc[(size_t)c * P + p];
@@ -1319,18 +1332,26 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
     if (id < -1) {  // an analytic sphere (spt_scene_set_spheres): -2 - k
         const uint32_t k = (uint32_t)(-2 - id);
         if (k >= a.sc.nsph) return;
-        const float4 sp = a.sc.spheres[k];
-        const V3 p = v3(a.ox[i] + t * a.dx[i], a.oy[i] + t * a.dy[i], a.oz[i] + t * a.dz[i]);
-        const V3 n = normalize(v3(p.x - sp.x, p.y - sp.y, p.z - sp.z));
-        if (a.px) a.px[i] = p.x;
-        if (a.py) a.py[i] = p.y;
-        if (a.pz) a.pz[i] = p.z;
-        if (a.gnx) a.gnx[i] = n.x;
-        if (a.gny) a.gny[i] = n.y;
-        if (a.gnz) a.gnz[i] = n.z;
-        if (a.snx) a.snx[i] = n.x;
-        if (a.sny) a.sny[i] = n.y;
-        if (a.snz) a.snz[i] = n.z;
+        // the hit point (and from it the normal) only when an output needs it:
+        // texcoord / material outputs never read the ray planes, which may be
+        // NULL then (spt_hit_info_compute checks the rest)
+        const bool want_n = a.gnx || a.gny || a.gnz || a.snx || a.sny || a.snz;
+        if (want_n || a.px || a.py || a.pz) {
+            const float4 sp = a.sc.spheres[k];
+            const V3 p = v3(a.ox[i] + t * a.dx[i], a.oy[i] + t * a.dy[i], a.oz[i] + t * a.dz[i]);
+            if (a.px) a.px[i] = p.x;
+            if (a.py) a.py[i] = p.y;
+            if (a.pz) a.pz[i] = p.z;
+            if (want_n) {
+                const V3 n = normalize(v3(p.x - sp.x, p.y - sp.y, p.z - sp.z));
+                if (a.gnx) a.gnx[i] = n.x;
+                if (a.gny) a.gny[i] = n.y;
+                if (a.gnz) a.gnz[i] = n.z;
+                if (a.snx) a.snx[i] = n.x;
+                if (a.sny) a.sny[i] = n.y;
+                if (a.snz) a.snz[i] = n.z;
+            }
+        }
         if (a.tcu) a.tcu[i] = 0.0f;
         if (a.tcv) a.tcv[i] = 0.0f;
         if (a.mat_id) a.mat_id[i] = a.sc.sph_mat ? a.sc.sph_mat[k] : 0;
@@ -1526,19 +1547,20 @@ hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s
 }
 
 hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
-                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, uint32_t order, hipStream_t s) {
+                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, uint32_t order,
+                          unsigned long long* unwritten, hipStream_t s) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(resolve_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sfilm, acc, out, P, nsamples,
-                       first_chunk, last_chunk, spp, order);
+                       first_chunk, last_chunk, spp, order, unwritten);
     return hipGetLastError();
 }
 
 hipError_t launch_resolve_flags(const uint8_t* sflag, float* acc, float* out, uint32_t P, uint32_t nsamples,
                                 uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, float env_r, float env_g,
-                                float env_b, uint32_t order, hipStream_t s) {
+                                float env_b, uint32_t order, unsigned long long* unwritten, hipStream_t s) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(resolve_flags_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, s, sflag, acc, out, P, nsamples,
-                       first_chunk, last_chunk, spp, env_r, env_g, env_b, order);
+                       first_chunk, last_chunk, spp, env_r, env_g, env_b, order, unwritten);
     return hipGetLastError();
 }
 

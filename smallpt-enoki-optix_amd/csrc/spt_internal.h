@@ -46,6 +46,11 @@ enum PathMode : int {
 };
 SPT_HD uint32_t mode_planes(int mode) { return mode == kModeUnit ? 2u : mode == kModeAlbedo ? 3u : 4u; }
 SPT_HD uint32_t mode_film_bytes(int mode) { return mode == kModeUnit ? 1u : 12u; }
+// Film slots are filled with 0xff bytes before a chunk renders (spt_render):
+// no path writes these values (a flag is 0 or 1; 0xffffffff is a NaN no
+// arithmetic produces), so the resolve can count slots nothing wrote.
+constexpr uint32_t kFlagSentinel = 0xffu;
+constexpr uint32_t kFilmSentinel = 0xffffffffu;
 
 // Path queue: planes of 16-B quads grouped by who reads them, so a kernel
 // moves a path in a few dwordx4 accesses (one coalesced 1-KB wave instruction
@@ -378,12 +383,15 @@ hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
 hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out);
 hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);
+// Both count the film slots still holding the pre-render sentinel (never
+// written: a lost path) into *unwritten.
 hipError_t launch_resolve(const float* sfilm, float* acc, float* out, uint32_t P, uint32_t nsamples,
-                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, uint32_t order, hipStream_t s);
+                          uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, uint32_t order,
+                          unsigned long long* unwritten, hipStream_t s);
 // unit mode: film = env added once per escaped sample, in sample order
 hipError_t launch_resolve_flags(const uint8_t* sflag, float* acc, float* out, uint32_t P, uint32_t nsamples,
                                 uint32_t first_chunk, uint32_t last_chunk, uint32_t spp, float env_r, float env_g,
-                                float env_b, uint32_t order, hipStream_t s);
+                                float env_b, uint32_t order, unsigned long long* unwritten, hipStream_t s);
 hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s);
 
 }  // namespace spt

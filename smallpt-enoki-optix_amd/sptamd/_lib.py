@@ -30,7 +30,7 @@ SPT_BUILD_AUTO, SPT_BUILD_HOST_SAH, SPT_BUILD_GPU_PLOC = 0, 1, 2
 EXPORTED = [
     "spt_init", "spt_scene_create", "spt_scene_create_ex", "spt_scene_set_albedo", "spt_scene_set_emission", "spt_scene_get_stats",
     "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
-    "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version",
+    "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version", "spt_build_id",
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write", "spt_pbrt_load",
     "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
     "spt_bvh_build_stats", "spt_scene_set_texture", "spt_scene_set_spheres", "spt_scene_set_material_kinds",
@@ -86,10 +86,14 @@ class RenderStats(ctypes.Structure):
                 ("isect_nodes", c_uint64), ("isect_tris", c_uint64), ("isect_lane_steps", c_uint64),
                 ("isect_wave_steps", c_uint64), ("isect_launches", c_uint64), ("streams", c_uint32),
                 ("fused", c_uint32), ("isect_busy_ms", c_double),
-                ("isect_max_stack", c_uint64)]
+                ("isect_max_stack", c_uint64),
+                ("paths_started", c_uint64), ("paths_terminated", c_uint64), ("film_slots_unwritten", c_uint64),
+                ("work_order", c_uint32), ("reserved0", c_uint32)]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        d = {name: getattr(self, name) for name, _ in self._fields_}
+        d.pop("reserved0")
+        return d
 
 
 class SceneStats(ctypes.Structure):
@@ -158,6 +162,7 @@ def _load() -> ctypes.CDLL:
         "spt_default_params": (None, [POINTER(RenderParams)]),
         "spt_last_error": (c_char_p, []),
         "spt_version": (c_char_p, []),
+        "spt_build_id": (c_char_p, []),
         "spt_obj_load": (i32, [c_char_p, POINTER(Mesh)]),
         "spt_mesh_free": (None, [POINTER(Mesh)]),
         "spt_pbrt_load": (i32, [c_char_p, POINTER(Mesh), POINTER(PbrtInfo)]),

@@ -197,6 +197,10 @@ class HipBackend:
             cap = n.value
         cfg = Config()
         check(lib.spt_scene_get_config(self._scene, ctypes.byref(cfg)), "spt_scene_get_config")
+        if self.base_config is None:
+            # the file's saved knobs are the base the SPT_* overrides apply to
+            # (not the library defaults, which would silently replace them)
+            self.base_config = Config.from_buffer_copy(bytes(cfg))
         self._applied = bytes(cfg)
         self._env_key = None
         st = SceneStats()

@@ -28,3 +28,21 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def assert_work_complete(st, rows, width, spp):
+    """spt_render_stats' device-counted work (include/spt.h): every (sample,
+    pixel) of the tile started, ended and wrote its film slot exactly once —
+    the reference renders every pixel x sample (main.cpp:385-429)."""
+    want = rows * width * spp
+    assert st["paths_started"] == want, (st["paths_started"], want)
+    assert st["paths_terminated"] == want, (st["paths_terminated"], want)
+    assert st["film_slots_unwritten"] == 0, st["film_slots_unwritten"]
+    assert st["paths"] == want
+    assert want == 0 or st["work_order"] in (1, 2)
+
+
+def spaced_rows(height, n):
+    """n evenly spaced rows of [0, height) (first and last included)."""
+    import numpy as np
+    return np.unique(np.linspace(0, height - 1, n).round().astype(np.int32))

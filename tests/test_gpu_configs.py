@@ -1,9 +1,10 @@
 """BASELINE.json configs[2..4] at their full sizes on the GPU (configs[1] is
-tests/test_gpu_render.py::test_headline_config_properties): the whole image is
-rendered exactly as bench.py renders it, sampled rows are compared bit for bit
-with the CPU oracle, and size-independent properties are checked on the rest
-(finite, non-negative; with albedo 1 and sky 1 every value a multiple of
-1/spp in [0, 1])."""
+tests/test_gpu_render.py::test_headline_config_whole_image): the whole image is
+rendered exactly as bench.py renders it, 64 evenly spaced rows are compared
+bit for bit with the CPU oracle, the device's work accounting must show every
+(sample, pixel) path started, ended and written once, and size-independent
+properties are checked on the rest (finite, non-negative; with albedo 1 and
+sky 1 every value a multiple of 1/spp in [0, 1])."""
 import argparse
 import os
 import sys
@@ -14,6 +15,7 @@ import torch
 
 import oracle as O
 import sptamd
+from conftest import assert_work_complete, spaced_rows
 from sptamd import scenes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -42,11 +44,13 @@ def setup(config):
     return cfg, s, kw, alb, emi
 
 
-def run(config, rows):
+def run(config, nrows=64):
     cfg, s, kw, alb, emi = setup(config)
     W, H, spp, D = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
+    rows = spaced_rows(H, nrows)
     film, st = s.render(sptamd.make_params(W, H, spp, D, **kw))
     torch.cuda.synchronize()
+    assert_work_complete(st, H, W, spp)
     got = film[:, rows, :].cpu().numpy()
     whole = film
     assert bool(torch.isfinite(whole).all()) and bool((whole >= 0).all())
@@ -61,21 +65,21 @@ def run(config, rows):
 
 def test_config2_cornell_full_size():
     """1024^2 x 1024 spp, depth 10, Kd albedo, Ke light, roulette from cast 5."""
-    film, st, spp = run(2, [100, 700])
+    film, st, spp = run(2)
     assert st["ray_casts"] > 4 * st["paths"]          # the compaction stress case
     assert float(film.max()) > 0
 
 
 def test_config3_tiled_size_full():
     """4096^2 x 256 spp, depth 8 (the per-GPU tile at N = 1)."""
-    film, st, spp = run(3, [2048])
+    film, st, spp = run(3)
     f = film[:, ::64, :]
     assert bool(((f * spp) == torch.round(f * spp)).all()) and bool((f <= 1).all())
 
 
 def test_config4_city_pbrt_full_size():
     """10M triangles through the pbrt reader and the GPU builder, 1920x1080 x 64 spp."""
-    film, st, spp = run(4, [540])
+    film, st, spp = run(4)
     # the GPU build of 10M triangles, packed node layout included, stays a
     # fraction of a second (it once took 76 s in a quadratic packing loop)
     assert st["bvh"]["builder"] == 2 and st["bvh"]["build_ms"] < 3000

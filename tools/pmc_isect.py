@@ -56,21 +56,27 @@ def main(out, key, log, *paths):
     mean = {c: sum(v.values()) / max(len(v), 1) for c, v in per.items()}
     b = bench_line(log)
     roof = b["roofline"]
-    # casts per launch: the isect launches and the shade launches both run once per cast
+    # units per launch (ray casts for isect_queue_kernel, paths for the fused
+    # kernel): the bench line's algorithmic bytes per launch / bytes per unit
+    unit = "path" if roof.get("unit_of_work") == "path" else "cast"
     casts = roof["algorithmic_bytes_per_launch"] / roof["bytes_per_unit"]
     rec = {"kernel": kernel, "workload": b["config"]["workload"], "streams": b["config"]["streams"],
-           "casts_per_launch": casts, "dispatches": {c: len(v) for c, v in per.items()}, "per_launch": mean,
+           "pipeline": b["config"].get("pipeline"), "work_order": b["config"].get("work_order"),
+           # the library build the passes measured (spt_build_id): bench.py uses
+           # this entry only while the loaded libspt.so reports the same id
+           "build_id": roof.get("build_id"),
+           f"{unit}s_per_launch": casts, "dispatches": {c: len(v) for c, v in per.items()}, "per_launch": mean,
            "source": [os.path.relpath(p) for p in paths]}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         t = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
         rec["traffic_bytes_per_launch"] = t
-        rec["traffic_bytes_per_cast"] = t / casts
-        rec["read_bytes_per_cast"] = 2.0 * mean["FETCH_SIZE"] * 1024.0 / casts
-        rec["write_bytes_per_cast"] = mean["WRITE_SIZE"] * 1024.0 / casts
+        rec[f"traffic_bytes_per_{unit}"] = t / casts
+        rec[f"read_bytes_per_{unit}"] = 2.0 * mean["FETCH_SIZE"] * 1024.0 / casts
+        rec[f"write_bytes_per_{unit}"] = mean["WRITE_SIZE"] * 1024.0 / casts
         rec["traffic_correction"] = "reads x2 (gfx950 FETCH_SIZE half-count, MI355X_MICROARCH.md HBM); estimate"
     if "SQ_INSTS_VALU" in mean:
         rec["valu_insts_per_launch"] = mean["SQ_INSTS_VALU"]
-        rec["valu_insts_per_cast"] = mean["SQ_INSTS_VALU"] / casts
+        rec[f"valu_insts_per_{unit}"] = mean["SQ_INSTS_VALU"] / casts
     if "TCC_HIT_sum" in mean:
         rec["l2_hit_rate"] = mean["TCC_HIT_sum"] / max(1.0, mean["TCC_HIT_sum"] + mean.get("TCC_MISS_sum", 0.0))
     if "SQ_WAVE_CYCLES" in mean:
