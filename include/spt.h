@@ -135,6 +135,8 @@ typedef struct spt_render_stats {
                                       sentinel when the resolve read them */
     uint32_t work_order;        /* the order that ran: SPT_WORK_SAMPLE_MAJOR or SPT_WORK_PIXEL_MAJOR */
     uint32_t reserved0;
+    uint64_t isect_tri_wave_steps;  /* SPT_FLAG_TRAVERSAL_STATS: wave steps in which some lane tested a triangle */
+    uint64_t isect_node_wave_steps; /*   ... in which some lane visited a node */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

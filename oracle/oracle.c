@@ -32,6 +32,15 @@
  *   ORACLE_ALT_TRI        Moller-Trumbore (not watertight) instead of the Woop
  *                         test standing in for OptiX's triangle test (optix_backend.h:314)
  *   (all)                 the four together
+ *   ORACLE_ALT_ENOKI      (separately) Enoki's own op forms on the CUDA backend, as
+ *                         its published headers define them: dot = an fmadd chain
+ *                         (x*x, then fma y, then fma z), Matrix x Array = an fmadd
+ *                         chain over the columns (coordframe.h:42,47 to_local /
+ *                         to_world: bx*l.x, fma by*l.y, fma bz*l.z), normalize =
+ *                         v * rsqrt(|v|^2) with the reciprocal square root
+ *                         correctly rounded (rsqrt.approx's own bits are NVIDIA's),
+ *                         and .ftz arithmetic (denormal inputs / results flushed
+ *                         to zero: MXCSR FTZ+DAZ in the worker threads)
  *   ORACLE_ALT_TEX1X1     (separately) every material's constant colour through
  *                         ImageTexture::eval as the reference's 1x1 image
  *                         (main.cpp:40-44, 62-76): bilinear weights that sum to
@@ -41,6 +50,9 @@
 
 #include <math.h>
 #include <pthread.h>
+#ifdef ORACLE_ALT_ENOKI
+#include <xmmintrin.h>
+#endif
 #include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
@@ -114,13 +126,22 @@ void oracle_sincos(float x, float* s_out, float* c_out) {
 typedef struct { float x, y, z; } v3;
 static inline v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
 static inline v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+#ifdef ORACLE_ALT_ENOKI
+/* Enoki dot: coeff(0) * coeff(0), then fmadd of each further coefficient */
+static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+#else
 static inline float dot3(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+#endif
 static inline v3 cross3(v3 a, v3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 /* Enoki normalize: v * rsqrt(squared_norm(v)); restated as v * (1/sqrt). */
 static inline v3 normalize3(v3 v) {
+#ifdef ORACLE_ALT_ENOKI
+    float inv = (float)(1.0 / sqrt((double)dot3(v, v)));  /* one rounding: rsqrt, not 1 / sqrt */
+#else
     float inv = 1.0f / sqrtf(dot3(v, v));
+#endif
 #ifdef ORACLE_ALT_RSQRT
     inv = nextafterf(inv, INFINITY);
 #endif
@@ -131,9 +152,16 @@ static inline float get(v3 v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : v.z
 /* Frame3 (coordframe.h:5-51): columns bx, by, bz; to_world = M * l. */
 typedef struct { v3 bx, by, bz; } frame3;
 static inline v3 to_world(const frame3* f, v3 l) {
+#ifdef ORACLE_ALT_ENOKI
+    /* Matrix x Array over the columns bx, by, bz (coordframe.h:47) */
+    return mk(fmaf(f->bz.x, l.z, fmaf(f->by.x, l.y, f->bx.x * l.x)),
+              fmaf(f->bz.y, l.z, fmaf(f->by.y, l.y, f->bx.y * l.x)),
+              fmaf(f->bz.z, l.z, fmaf(f->by.z, l.y, f->bx.z * l.x)));
+#else
     return mk((f->bx.x * l.x + f->by.x * l.y) + f->bz.x * l.z,
               (f->bx.y * l.x + f->by.y * l.y) + f->bz.y * l.z,
               (f->bx.z * l.x + f->by.z * l.y) + f->bz.z * l.z);
+#endif
 }
 static inline v3 to_local(const frame3* f, v3 w) {
     return mk(dot3(f->bx, w), dot3(f->by, w), dot3(f->bz, w));
@@ -715,12 +743,19 @@ typedef struct {
 } pfor_t;
 static void* pfor_worker(void* arg) {
     pfor_t* p = (pfor_t*)arg;
+#ifdef ORACLE_ALT_ENOKI
+    const unsigned int csr = _mm_getcsr();
+    _mm_setcsr(csr | 0x8040u);  /* FTZ + DAZ: PTX .ftz */
+#endif
     for (;;) {
         int64_t b = atomic_fetch_add(&p->next, p->chunk);
         if (b >= p->n) break;
         int64_t e = b + p->chunk < p->n ? b + p->chunk : p->n;
         for (int64_t i = b; i < e; i++) p->fn(p->ctx, i);
     }
+#ifdef ORACLE_ALT_ENOKI
+    _mm_setcsr(csr);  /* the caller's thread (nthreads <= 1) gets its mode back */
+#endif
     return NULL;
 }
 static void parallel_for(int64_t n, int64_t chunk, int nthreads, void (*fn)(void*, int64_t), void* ctx) {

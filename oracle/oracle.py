@@ -32,7 +32,7 @@ def build() -> str:
 
 
 # oracle.c header: one unpinned arithmetic choice each, and all four at once
-VARIANTS = ("sincos", "rsqrt", "fma", "tri", "all", "tex1x1")
+VARIANTS = ("sincos", "rsqrt", "fma", "tri", "all", "tex1x1", "enoki")
 
 
 def _load(path=LIB_PATH):

@@ -86,7 +86,8 @@ struct Counters {
 // Render-wide device statistics.
 struct Stats {
     unsigned long long stats[3];  // casts, continuations, camera rays started
-    unsigned long long trav[5];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps, max stack
+    unsigned long long trav[7];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps, max stack,
+                                  // wave steps running the triangle block, the visit block
     unsigned long long unwritten; // film slots still holding the sentinel at resolve time
 };
 
@@ -1814,7 +1815,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     }
     // pinned destination: a pageable one makes the copy a staged, slower transfer
     const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(ws.host_stats);
-    static_assert(sizeof(Stats) == 9 * sizeof(unsigned long long), "Stats is the 9 counters read back here");
+    static_assert(sizeof(Stats) == 11 * sizeof(unsigned long long), "Stats is the 11 counters read back here");
     HIP_TRY(hipMemcpyAsync(ws.host_stats, ws.stats, sizeof(Stats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     rs.ray_casts = hstats[0];
@@ -1829,7 +1830,9 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     rs.paths_started = hstats[2];
     rs.paths_terminated = hstats[0] - hstats[1];  // every cast either continues or ends its path
     rs.paths = rs.paths_terminated;
-    rs.film_slots_unwritten = hstats[8];
+    rs.film_slots_unwritten = hstats[10];
+    rs.isect_tri_wave_steps = hstats[8];
+    rs.isect_node_wave_steps = hstats[9];
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
     if (timing) {
         uint64_t nis = 0;

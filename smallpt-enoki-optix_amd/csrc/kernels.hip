@@ -25,6 +25,47 @@ __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
 #endif
 }
 
+// Path-queue and hit-record accesses: each element is read or written once
+// per cast, so with SPT_NT_QUEUE they bypass cache retention (non-temporal)
+// and leave L2 / Infinity Cache to the BVH nodes and triangles.
+#ifndef SPT_NT_QUEUE
+#define SPT_NT_QUEUE 0
+#endif
+typedef float spt_f4v __attribute__((ext_vector_type(4)));
+typedef float spt_f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ldq(const float4* p) {
+#if SPT_NT_QUEUE
+    const spt_f4v v = __builtin_nontemporal_load((const spt_f4v*)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stq(float4* p, float4 x) {
+#if SPT_NT_QUEUE
+    spt_f4v v = {x.x, x.y, x.z, x.w};
+    __builtin_nontemporal_store(v, (spt_f4v*)p);
+#else
+    *p = x;
+#endif
+}
+__device__ __forceinline__ float2 ldq2(const float2* p) {
+#if SPT_NT_QUEUE
+    const spt_f2v v = __builtin_nontemporal_load((const spt_f2v*)p);
+    return make_float2(v.x, v.y);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stq2(float2* p, float2 x) {
+#if SPT_NT_QUEUE
+    spt_f2v v = {x.x, x.y};
+    __builtin_nontemporal_store(v, (spt_f2v*)p);
+#else
+    *p = x;
+#endif
+}
+
 // minimum waves per SIMD the isect kernels are compiled for (register budget)
 #ifndef SPT_ISECT_WAVES
 #define SPT_ISECT_WAVES 1
@@ -94,14 +135,26 @@ struct NoStats {
     __device__ void tri() {}
     __device__ void step() {}
     __device__ void push(uint32_t) {}
+    __device__ void wave_blocks(bool, bool) {}
 };
 struct TravStats {
     uint32_t nodes = 0, tris = 0, steps = 0, max_sp = 0, empties = 0;
+    uint32_t tri_waves = 0, node_waves = 0;  // wave steps that ran the triangle / the visit block
     __device__ void empty_visit() { empties++; }
     __device__ void node() { nodes++; }
     __device__ void tri() { tris++; }
     __device__ void step() { steps++; }
     __device__ void push(uint32_t sp) { max_sp = max(max_sp, sp); }
+    // called by every stepping lane: whether any stepping lane of the wave
+    // tests a triangle / visits a node in this step (the SIMD pays the
+    // block); the lowest stepping lane counts it, so lane sums are exact
+    __device__ void wave_blocks(bool tri_lane, bool node_lane) {
+        const uint64_t act = __ballot(true), bt = __ballot(tri_lane), bn = __ballot(node_lane);
+        if (lane_id() == (uint32_t)__ffsll((unsigned long long)act) - 1u) {
+            tri_waves += bt != 0 ? 1u : 0u;
+            node_waves += bn != 0 ? 1u : 0u;
+        }
+    }
 };
 
 // Stack-based BVH2 traversal, near child first, stack in LDS at
@@ -553,6 +606,7 @@ struct Tracer8T {
         const uint32_t bit = 31u - (uint32_t)__builtin_clz(nhits | 1u);
         const uint32_t child = ((nhits & 0x00ffffffu) << sc.group_shift) + (((bit - 24u) ^ oct_rep) & 7u);
         const uint32_t node = do_node ? child : 0u;
+        stats.wave_blocks(has_tri, do_node);
         if (do_node) {
             stats.node();
             nhits &= ~(1u << bit);
@@ -682,7 +736,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
                 if (!busy && rank < take) {
                     ray = pool + rank;
-                    const float4 q1 = a.q.q1[ray], q2 = a.q.q2[ray];
+                    const float4 q1 = ldq(a.q.q1 + ray), q2 = ldq(a.q.q2 + ray);
                     const V3 o = v3(q1.x, q1.y, q1.z);
                     const V3 d = v3(q2.x, q2.y, q2.z);
                     const uint32_t depth = f2u(q1.w) & ((1u << kMetaDepthBits) - 1u);
@@ -691,7 +745,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
                     busy = !tr.finished();
                     if (!busy) {  // empty scene: the miss record init made
                         const TraceHit hh = tr.hit(a.sc, L);
-                        a.hits[ray] = make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v);
+                        stq(a.hits + ray, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
                     }
                 }
                 pool += take;
@@ -702,7 +756,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
         wave_steps++;
         if (busy && tr.step(a.sc, L, st)) {
             const TraceHit hh = tr.hit(a.sc, L);
-            a.hits[ray] = make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v);
+            stq(a.hits + ray, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
             busy = false;
         }
     }
@@ -711,6 +765,8 @@ void isect_queue_kernel(IsectQueueArgs a) {
         atomicAdd(&a.trav_stats[1], (unsigned long long)st.tris);
         atomicAdd(&a.trav_stats[2], (unsigned long long)st.steps);
         if ((threadIdx.x & 63u) == 0) atomicAdd(&a.trav_stats[3], (unsigned long long)wave_steps);
+        atomicAdd(&a.trav_stats[5], (unsigned long long)st.tri_waves);
+        atomicAdd(&a.trav_stats[6], (unsigned long long)st.node_waves);
 #if SPT_EMPTY_VISIT_STAT
         atomicAdd(&a.trav_stats[4], (unsigned long long)st.empties);  // experiment: visits with no child hit
 #else
@@ -833,10 +889,10 @@ __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32
 template <int kMode>
 __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix, uint32_t meta,
                                            float tr, float tg, float tb, float lr, float lg, float lb) {
-    q.q1[j] = make_float4(o.x, o.y, o.z, u2f(meta));
-    q.q2[j] = make_float4(d.x, d.y, d.z, u2f(pix));
-    if (kMode >= kModeAlbedo) q.q0[j] = make_float4(tr, tg, tb, kMode == kModeEmit ? lr : 0.0f);
-    if (kMode == kModeEmit) q.rad[j] = make_float2(lg, lb);
+    stq(q.q1 + j, make_float4(o.x, o.y, o.z, u2f(meta)));
+    stq(q.q2 + j, make_float4(d.x, d.y, d.z, u2f(pix)));
+    if (kMode >= kModeAlbedo) stq(q.q0 + j, make_float4(tr, tg, tb, kMode == kModeEmit ? lr : 0.0f));
+    if (kMode == kModeEmit) stq2(q.rad + j, make_float2(lg, lb));
 }
 
 // PCG32 of global pixel gpix (main.cpp:376) advanced past the draws a path
@@ -934,12 +990,12 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     }
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     if (i < n) {
-        const float4 q1 = a.in.q1[i], q2 = a.in.q2[i];
+        const float4 q1 = ldq(a.in.q1 + i), q2 = ldq(a.in.q2 + i);
         meta = f2u(q1.w);
         pix = f2u(q2.w);
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
-        hit = a.hits[i];
+        hit = ldq(a.hits + i);
         slot = (int32_t)f2u(hit.x);
         if (kSpt && a.sc.nsph) {
             // smallpt's analytic spheres after the triangle BVH (the isect kernel
@@ -952,11 +1008,11 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             hit = make_float4(u2f((uint32_t)slot), h.t, h.u, h.v);
         }
         if (kMode >= kModeAlbedo) {
-            const float4 q0 = a.in.q0[i];
+            const float4 q0 = ldq(a.in.q0 + i);
             tr = q0.x; tg = q0.y; tb = q0.z;
             if (kMode == kModeEmit) lr = q0.w;
         }
-        if (kMode == kModeEmit) { const float2 l = a.in.rad[i]; lg = l.x; lb = l.y; }
+        if (kMode == kModeEmit) { const float2 l = ldq2(a.in.rad + i); lg = l.x; lb = l.y; }
         bool term = true, escaped = false;
         if (slot == -1) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)

@@ -42,4 +42,10 @@ def test_bench_ranks_match_one_rank(tmp_path, n):
                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(n),
                 *SMALL, "--save", str(tmp_path / "n.npy")], env)
     assert rec["n_gpus"] == n and rec["value"] > 0
+    assert rec["dist"] == {"backend": "gloo", "world_size": n}
+    assert rec["work_check"]["paths_device_counted"] == rec["work_check"]["expected"] == 256 * 128 * 4
+    # a tile of this size runs fused (AUTO): the north-star wavefront is timed beside it
+    assert rec["config"]["pipeline"] == "fused" and rec["roofline"]["unit_of_work"] == "path"
+    leg = rec["wavefront_leg"]
+    assert leg["value"] > 0 and leg["paths_device_counted"] == 256 * 128 * 4 and leg["image_equal_to_fused"]
     np.testing.assert_array_equal(np.load(tmp_path / "n.npy"), np.load(tmp_path / "one.npy"))

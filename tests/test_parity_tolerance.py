@@ -11,6 +11,10 @@ oracle again with each choice swapped (oracle.c header):
                                                        Frame3 coordframe.h:40-48, dots, camera)
   tri     Moller-Trumbore instead of the Woop test     (OptiX's test, optix_backend.h:314)
   all     the four together
+  tex1x1  constant colours through a 1x1 ImageTexture  (main.cpp:40-44, 62-76)
+  enoki   Enoki's own op forms on its CUDA backend: fmadd-chain dot and
+          Matrix x Array (coordframe.h:42,47), a correctly rounded rsqrt in
+          normalize, .ftz (denormals flushed)
 
 and these tests bound the image change against the build's image on the
 BASELINE configs[0] shape, a deeper one and the reference's default run.
@@ -100,3 +104,14 @@ def test_variants_are_live():
     a = O.OracleScene(m).intersect(oo, dd)
     b = O.OracleScene(m, lib=O.variant("tri")).intersect(oo, dd)
     assert np.array_equal(a[0], b[0]) and not np.array_equal(a[2], b[2])  # same hits, other bits
+    # enoki: Frame3::to_world as an fmadd chain over the columns changes bits
+    nn = rng.normal(size=(500, 3)).astype(np.float32)
+    ll = rng.uniform(0.0, 1.0, size=(500, 3)).astype(np.float32)
+    base = np.array([O.frame_to_world(n, l) for n, l in zip(nn, ll)])
+    alt = []
+    for n, l in zip(nn, ll):
+        out = np.zeros(3, np.float32)
+        O.variant("enoki").oracle_frame_to_world(n.ctypes.data, l.ctypes.data, out.ctypes.data)
+        alt.append(out)
+    alt = np.array(alt)
+    assert not np.array_equal(base, alt) and np.allclose(base, alt, rtol=1e-5, atol=1e-6)

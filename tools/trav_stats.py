@@ -60,6 +60,11 @@ def main():
                "tris_per_ray": round(ss["isect_tris"] / casts, 2),
                "steps_per_ray": round(ss["isect_lane_steps"] / casts, 2),
                "simd_eff": round(ss["isect_lane_steps"] / (64.0 * ss["isect_wave_steps"]), 3),
+               # the blocks the SIMD runs: fraction of wave steps, and lanes using them when run
+               "tri_block_frac": round(ss["isect_tri_wave_steps"] / max(1, ss["isect_wave_steps"]), 3),
+               "node_block_frac": round(ss["isect_node_wave_steps"] / max(1, ss["isect_wave_steps"]), 3),
+               "tri_block_lanes": round(ss["isect_tris"] / max(1, ss["isect_tri_wave_steps"]), 2),
+               "node_block_lanes": round(ss["isect_nodes"] / max(1, ss["isect_node_wave_steps"]), 2),
                "max_stack": ss["isect_max_stack"]}
         print(json.dumps(rec), flush=True)
 
