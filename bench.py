@@ -269,43 +269,54 @@ def main():
                                f"expected {want} paths")
         return want
 
-    def step(p, timed=False, evs=None):
-        _, st = scene.render(p, film=film, stream=stream)
-        if timed:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+    # gather timing events, created once (recorded on the render stream)
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(max(args.steps, 1))]
+
+    def step(p, i=None):
+        """One step: the render of this rank's tile, queued (spt_render_async:
+        the GPU runs from one step's render into the next without waiting for
+        the host), then the tile gather on the same stream.  Returns the
+        render's ticket; its device counters are collected after the loop."""
+        _, ticket = scene.render_async(p, film=film, stream=stream)
+        if i is not None:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
+            gev[i][0].record(stream)
         tg.gather()
-        if timed:
-            e1.record(stream)
-            evs.append((e0, e1))
-        return st
+        if i is not None:
+            gev[i][1].record(stream)
+            gather_ev.append(gev[i])
+        return ticket
 
     def timed_loop(p, evs):
         """W untimed steps, then exactly K timed steps between barriers +
         synchronize; returns (max-over-ranks seconds, summed stats, last stats,
-        device-counted paths of all ranks)."""
+        device-counted paths of all ranks).  Every step's work accounting is
+        checked once the timed region has ended."""
         for _ in range(args.warmup):
-            check_work(step(p))
+            check_work(scene.render_wait(step(p)))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        evs.clear()
         t0 = time.perf_counter()
-        agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
-               "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0,
-               "paths": 0}
-        sts = []
-        for _ in range(args.steps):
-            st = step(p, timed=True, evs=evs)
-            sts.append(st)
-            for k in agg:
-                agg[k] += st[k]
+        tickets, sts = [], []
+        for i in range(args.steps):
+            tickets.append(step(p, i))
+            if len(tickets) > 32:  # the library holds at most 64 uncollected renders
+                sts.append(scene.render_wait(tickets.pop(0)))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        for st in sts:  # after the timed region: the counters were read back by every render anyway
+        agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
+               "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0,
+               "paths": 0}
+        sts += [scene.render_wait(t) for t in tickets]
+        for st in sts:
             check_work(st)
+            for k in agg:
+                agg[k] += st[k]
         tot = [agg["ray_casts"], agg["continuations"], agg["paths"]]
         if world > 1:
             rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
@@ -328,7 +339,9 @@ def main():
     if world > 1 and st.get("fused") and args.pipeline == "auto":
         pw = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
                                 wavefront_paths=args.wavefront, timing=True, pipeline="wavefront", **kw)
-        w_el, w_agg, w_st, w_tot = timed_loop(pw, [])
+        main_gather = list(gather_ev)
+        w_el, w_agg, w_st, w_tot = timed_loop(pw, gather_ev)
+        gather_ev[:] = main_gather
         w_paths = w_tot[2]
         wave_leg = {"pipeline": "wavefront", "value": round(w_paths / w_el / 1e6, 3),
                     "ms_per_step": round(w_el / args.steps * 1e3, 3), "streams": w_st.get("streams"),

@@ -386,6 +386,23 @@ spt_status spt_hit_info_compute(spt_scene scene, const spt_rays* rays, const spt
 spt_status spt_render(spt_scene scene, const spt_render_params* params, float* film_dev,
                       spt_render_stats* stats, void* stream);
 
+/* spt_render in two halves, so that renders can be queued back to back: the
+ * GPU then runs one frame into the next with no gap for the host's return,
+ * the caller's own work between frames, and the next call's set-up
+ * (the reference's host loop likewise only queues work, main.cpp:385-429).
+ * spt_render_async queues the whole render of `params` on `stream` and returns
+ * a ticket; its host loop still follows the wavefront's queue counters while
+ * the render runs, so the call returns near the end of the render's GPU work,
+ * not at its start.  The film is complete once the stream reaches the point
+ * where the call returned.  spt_render_wait(ticket) waits for that render and
+ * fills its statistics (stats may be NULL); every ticket must be collected
+ * once, and at most 64 renders of a scene may be queued without being
+ * collected (SPT_ERR_LIMIT).  spt_render(...) = spt_render_async +
+ * spt_render_wait. */
+spt_status spt_render_async(spt_scene scene, const spt_render_params* params, float* film_dev, void* stream,
+                            uint64_t* ticket);
+spt_status spt_render_wait(spt_scene scene, uint64_t ticket, spt_render_stats* stats);
+
 /* Rows of tile `tile_index` (in increasing order).  Returns the row count;
  * writes at most `cap` row indices into rows (may be NULL). */
 uint32_t spt_tile_rows(uint32_t height, uint32_t tile_index, uint32_t tile_count,

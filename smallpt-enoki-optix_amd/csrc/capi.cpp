@@ -93,6 +93,25 @@ struct Stats {
 
 constexpr int kMaxStreams = 4;
 
+// One render's own state, so that renders can be queued back to back
+// (spt_render_async) while earlier ones are still on the GPU: its device
+// counters and their pinned readback, its timing events, and the host-side
+// statistics known at enqueue time.  The workspace keeps a ring of them.
+constexpr int kRenderSlots = 64;
+struct RenderSlot {
+    Stats* dev = nullptr;                       // device counters of this render
+    Stats* host = nullptr;                      // pinned readback, complete once `done` has fired
+    std::vector<hipEvent_t> events;             // [0] = time origin, then start/end pairs of timed launches
+    std::vector<std::pair<size_t, int>> timed;  // (start event index, 0 refill 1 isect 2 shade 3 resolve)
+    hipEvent_t done = nullptr;                  // recorded after the readback
+    spt_render_stats rs{};                      // fields known when the render was queued
+    uint64_t regen_base = 0;                    // camera rays of the first launch (for rs.regenerations)
+    bool timing = false;
+    double wall0 = 0.0;
+    uint64_t ticket = 0;
+    bool pending = false;                       // queued, not yet collected by spt_render_wait
+};
+
 // One sub-wavefront: its own double-buffered path queue, hit records and
 // counters, driven on its own stream so its launch tails overlap the others'.
 struct Sub {
@@ -116,10 +135,9 @@ struct Workspace {
     float* acc = nullptr;               // [3][P] running sum across chunks
     PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
-    Stats* stats = nullptr;
-    Stats* host_stats = nullptr;        // pinned readback of stats
+    RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
+    uint64_t next_ticket = 1;
     hipEvent_t fork_ev = nullptr;
-    std::vector<hipEvent_t> events;
 
     void release() {
         for (Sub& b : sub) {
@@ -129,11 +147,17 @@ struct Workspace {
             if (b.join_ev) (void)hipEventDestroy(b.join_ev);
             if (b.stream) (void)hipStreamDestroy(b.stream);
         }
-        hfree(film); hfree(acc); hfree(jumps); hfree(stats);
-        if (host_stats) (void)hipHostFree(host_stats);
+        hfree(film); hfree(acc); hfree(jumps);
+        for (RenderSlot& r : slots) {
+            hfree(r.dev);
+            if (r.host) (void)hipHostFree(r.host);
+            for (auto e : r.events) (void)hipEventDestroy(e);
+            if (r.done) (void)hipEventDestroy(r.done);
+        }
         if (fork_ev) (void)hipEventDestroy(fork_ev);
-        for (auto e : events) (void)hipEventDestroy(e);
+        const uint64_t t = next_ticket;  // tickets stay unique over the scene's life
         *this = Workspace();
+        next_ticket = t;
     }
 };
 
@@ -273,19 +297,93 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, u
         HIP_TRY(hipMalloc((void**)&ws.jumps, sizeof(PcgJump) * njumps));
         ws.jump_cap = njumps;
     }
-    if (!ws.stats) HIP_TRY(hipMalloc((void**)&ws.stats, sizeof(Stats)));
-    if (!ws.host_stats) HIP_TRY(hipHostMalloc((void**)&ws.host_stats, sizeof(Stats), hipHostMallocDefault));
     if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
     return SPT_OK;
 }
 
-spt_status get_event(Workspace& ws, size_t idx, hipEvent_t* out) {
-    while (ws.events.size() <= idx) {
+spt_status get_event(RenderSlot& r, size_t idx, hipEvent_t* out) {
+    while (r.events.size() <= idx) {
         hipEvent_t e;
         HIP_TRY(hipEventCreate(&e));
-        ws.events.push_back(e);
+        r.events.push_back(e);
     }
-    *out = ws.events[idx];
+    *out = r.events[idx];
+    return SPT_OK;
+}
+
+// The slot of the next render; SPT_ERR_LIMIT when the render kRenderSlots
+// tickets earlier was never collected.
+spt_status render_slot(Workspace& ws, RenderSlot** out) {
+    RenderSlot& r = ws.slots[ws.next_ticket % kRenderSlots];
+    if (r.pending)
+        return fail(SPT_ERR_LIMIT, "spt_render_async: %d renders queued without spt_render_wait", kRenderSlots);
+    if (!r.dev) HIP_TRY(hipMalloc((void**)&r.dev, sizeof(Stats)));
+    if (!r.host) HIP_TRY(hipHostMalloc((void**)&r.host, sizeof(Stats), hipHostMallocDefault));
+    if (!r.done) HIP_TRY(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+    r.timed.clear();
+    r.rs = spt_render_stats{};
+    r.timing = false;
+    *out = &r;
+    return SPT_OK;
+}
+
+// Waits for a queued render and fills its statistics (device counters, the
+// union of its isect launch intervals, host wall time since it was queued).
+spt_status render_collect(RenderSlot& r, spt_render_stats* out) {
+    spt_render_stats rs = r.rs;
+    r.pending = false;
+    if (rs.tile_rows) {  // an empty tile queued nothing
+        HIP_TRY(hipEventSynchronize(r.done));
+        const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(r.host);
+        static_assert(sizeof(Stats) == 11 * sizeof(unsigned long long), "Stats is the 11 counters read back here");
+        rs.ray_casts = hstats[0];
+        rs.continuations = hstats[1];
+        rs.regenerations = hstats[2] > r.regen_base ? hstats[2] - r.regen_base : 0;
+        rs.isect_nodes = hstats[3];
+        rs.isect_tris = hstats[4];
+        rs.isect_lane_steps = hstats[5];
+        rs.isect_wave_steps = hstats[6];
+        rs.isect_max_stack = hstats[7];
+        rs.paths_started = hstats[2];
+        rs.paths_terminated = hstats[0] - hstats[1];  // every cast either continues or ends its path
+        rs.paths = rs.paths_terminated;
+        rs.film_slots_unwritten = hstats[10];
+        rs.isect_tri_wave_steps = hstats[8];
+        rs.isect_node_wave_steps = hstats[9];
+        if (r.timing) {
+            uint64_t nis = 0;
+            std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin
+            for (auto& tk : r.timed) {
+                float ms = 0.0f;
+                HIP_TRY(hipEventElapsedTime(&ms, r.events[tk.first], r.events[tk.first + 1]));
+                if (tk.second == 0) rs.camera_ms += ms;
+                else if (tk.second == 1) {
+                    rs.isect_ms += ms;
+                    nis++;
+                    float t0 = 0.0f;
+                    HIP_TRY(hipEventElapsedTime(&t0, r.events[0], r.events[tk.first]));
+                    iv.push_back({t0, t0 + ms});
+                } else if (tk.second == 2) rs.shade_ms += ms;
+                else rs.resolve_ms += ms;
+            }
+            rs.isect_launches = nis;
+            // launches on the K streams overlap: busy time = union of their intervals
+            std::sort(iv.begin(), iv.end());
+            float lo = 0.0f, hi = -1.0f;
+            for (auto& x : iv) {
+                if (x.first > hi) {
+                    if (hi > lo) rs.isect_busy_ms += hi - lo;
+                    lo = x.first;
+                    hi = x.second;
+                } else {
+                    hi = std::max(hi, x.second);
+                }
+            }
+            if (hi > lo) rs.isect_busy_ms += hi - lo;
+        }
+    }
+    rs.total_ms = now_ms() - r.wall0;
+    if (out) *out = rs;
     return SPT_OK;
 }
 
@@ -1421,10 +1519,10 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
     return SPT_OK;
 }
 
-spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev, spt_render_stats* stats_out,
-                      void* stream_) {
+spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* film_dev, void* stream_,
+                            uint64_t* ticket_out) {
     const double wall0 = now_ms();
-    if (!sc || !pp) return fail(SPT_ERR_INVALID, "spt_render: NULL argument");
+    if (!sc || !pp || !ticket_out) return fail(SPT_ERR_INVALID, "spt_render: NULL argument");
     const spt_render_params& p = *pp;
     if (p.width == 0 || p.height == 0 || p.spp == 0 || p.max_depth == 0)
         return fail(SPT_ERR_INVALID, "spt_render: width/height/spp/max_depth must be > 0");
@@ -1438,14 +1536,20 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     hipStream_t stream = (hipStream_t)stream_;
     const uint32_t rows = spt_tile_rows(p.height, p.tile_index, p.tile_count, p.rows_per_group, nullptr, 0);
     const uint64_t P = (uint64_t)rows * p.width;
-    spt_render_stats rs{};
+    if (P != 0 && !film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
+    std::lock_guard<std::mutex> lock(sc->mu);  // the scene's one workspace
+    RenderSlot* slot = nullptr;
+    spt_status st = render_slot(sc->ws, &slot);
+    if (st) return st;
+    spt_render_stats& rs = slot->rs;
     rs.tile_rows = rows;
+    slot->wall0 = wall0;
     if (P == 0) {  // an empty tile: nothing to render, film untouched
-        if (stats_out) *stats_out = rs;
+        slot->ticket = sc->ws.next_ticket++;
+        slot->pending = true;
+        *ticket_out = slot->ticket;
         return SPT_OK;
     }
-    if (!film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
-    std::lock_guard<std::mutex> lock(sc->mu);  // the scene's one workspace
     const spt_config& cfg = sc->cfg;
 
     // Wavefront capacity.  Each isect launch ends in a tail where its last rays
@@ -1518,7 +1622,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
     rs.paths_in_flight = (uint32_t)C;
-    spt_status st = ensure_workspace(sc->ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P,
+    st = ensure_workspace(sc->ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P,
                                      3 * P, (size_t)p.spp + kMaxDepthCasts);
     if (st) return st;
     Workspace& ws = sc->ws;
@@ -1548,9 +1652,9 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     const auto resolve = [&](uint32_t s0, uint32_t ns) {
         return mode == kModeUnit
                    ? launch_resolve_flags(sflag, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                          p.env[0], p.env[1], p.env[2], film_order, &ws.stats->unwritten, stream)
+                                          p.env[0], p.env[1], p.env[2], film_order, &slot->dev->unwritten, stream)
                    : launch_resolve(sfilm, acc, film_dev, (uint32_t)P, ns, s0 == 0, s0 + ns >= p.spp, p.spp,
-                                    film_order, &ws.stats->unwritten, stream);
+                                    film_order, &slot->dev->unwritten, stream);
     };
     // every slot of a chunk starts as the sentinel (kFlagSentinel / kFilmSentinel
     // bytes), so the resolve counts slots no path wrote (spt_render_stats)
@@ -1559,22 +1663,23 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     };
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
-    HIP_TRY(hipMemsetAsync(ws.stats, 0, sizeof(Stats), stream));
+    HIP_TRY(hipMemsetAsync(slot->dev, 0, sizeof(Stats), stream));
     // time origin for the isect launch intervals (their union = isect busy time)
-    hipEvent_t origin_ev = nullptr;
+    slot->timing = timing;
     if (timing) {
-        if ((st = get_event(ws, 0, &origin_ev))) return st;
+        hipEvent_t origin_ev = nullptr;
+        if ((st = get_event(*slot, 0, &origin_ev))) return st;
         HIP_TRY(hipEventRecord(origin_ev, stream));
     }
 
-    std::vector<std::pair<size_t, int>> timed;  // (start event index, 0 refill 1 isect 2 shade 3 resolve)
+    std::vector<std::pair<size_t, int>>& timed = slot->timed;
     size_t ev = 1;  // events[0] is the origin
     auto mark = [&](int kind, hipStream_t sk, auto&& launch) -> spt_status {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         spt_status s2;
         const bool tm = kind == 1 ? timing : timing_all;
         if (tm) {
-            if ((s2 = get_event(ws, ev, &e0)) || (s2 = get_event(ws, ev + 1, &e1))) return s2;
+            if ((s2 = get_event(*slot, ev, &e0)) || (s2 = get_event(*slot, ev + 1, &e1))) return s2;
             HIP_TRY(hipEventRecord(e0, sk));
         }
         HIP_TRY(launch());
@@ -1599,7 +1704,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         I.sc = sc->dev();
         I.hits = (float4*)b.hits;
         I.max_depth = p.max_depth;
-        I.trav_stats = trav_stats ? ws.stats->trav : nullptr;
+        I.trav_stats = trav_stats ? slot->dev->trav : nullptr;
         I.next = &b.cnt->isect_next;
         // 24 idle lanes / a 1/2 static share: +1.5 % over 16 / 5/8 at the
         // 32M wavefront (tools/envsweep.sh, tools/envsweep_r01_v11.txt)
@@ -1626,7 +1731,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         RefillArgs& R = ra[k];
         R.cam = cam;
         R.sample_jump = ws.jumps;
-        R.stats = ws.stats->stats;
+        R.stats = slot->dev->stats;
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
         R.pixel_block = cfg.pixel_block;
@@ -1644,7 +1749,7 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         F.sample_jump = ws.jumps;
         F.sfilm = sfilm;
         F.sflag = sflag;
-        F.stats = ws.stats->stats;
+        F.stats = slot->dev->stats;
         F.next = &ws.sub[0].cnt->isect_next;
         F.initstate = p.rng_initstate;
         F.P = (uint32_t)P; F.W = p.width; F.max_depth = p.max_depth;
@@ -1814,62 +1919,35 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
         if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
     }
     // pinned destination: a pageable one makes the copy a staged, slower transfer
-    const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(ws.host_stats);
-    static_assert(sizeof(Stats) == 11 * sizeof(unsigned long long), "Stats is the 11 counters read back here");
-    HIP_TRY(hipMemcpyAsync(ws.host_stats, ws.stats, sizeof(Stats), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    rs.ray_casts = hstats[0];
-    rs.continuations = hstats[1];
-    rs.regenerations = hstats[2] > C ? hstats[2] - std::min<uint64_t>(C, P * p.spp) : 0;
+    HIP_TRY(hipMemcpyAsync(slot->host, slot->dev, sizeof(Stats), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipEventRecord(slot->done, stream));
     rs.iterations = iters;
-    rs.isect_nodes = hstats[3];
-    rs.isect_tris = hstats[4];
-    rs.isect_lane_steps = hstats[5];
-    rs.isect_wave_steps = hstats[6];
-    rs.isect_max_stack = hstats[7];
-    rs.paths_started = hstats[2];
-    rs.paths_terminated = hstats[0] - hstats[1];  // every cast either continues or ends its path
-    rs.paths = rs.paths_terminated;
-    rs.film_slots_unwritten = hstats[10];
-    rs.isect_tri_wave_steps = hstats[8];
-    rs.isect_node_wave_steps = hstats[9];
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
-    if (timing) {
-        uint64_t nis = 0;
-        std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin
-        for (auto& tk : timed) {
-            float ms = 0.0f;
-            HIP_TRY(hipEventElapsedTime(&ms, ws.events[tk.first], ws.events[tk.first + 1]));
-            if (tk.second == 0) rs.camera_ms += ms;
-            else if (tk.second == 1) {
-                rs.isect_ms += ms;
-                nis++;
-                float t0 = 0.0f;
-                HIP_TRY(hipEventElapsedTime(&t0, origin_ev, ws.events[tk.first]));
-                iv.push_back({t0, t0 + ms});
-            } else if (tk.second == 2) rs.shade_ms += ms;
-            else rs.resolve_ms += ms;
-        }
-        rs.isect_launches = nis;
-        // launches on the K streams overlap: busy time = union of their intervals
-        std::sort(iv.begin(), iv.end());
-        float lo = 0.0f, hi = -1.0f;
-        for (auto& x : iv) {
-            if (x.first > hi) {
-                if (hi > lo) rs.isect_busy_ms += hi - lo;
-                lo = x.first;
-                hi = x.second;
-            } else {
-                hi = std::max(hi, x.second);
-            }
-        }
-        if (hi > lo) rs.isect_busy_ms += hi - lo;
-    }
     rs.streams = (uint32_t)K;
     rs.fused = fused ? 1u : 0u;
-    rs.total_ms = now_ms() - wall0;
-    if (stats_out) *stats_out = rs;
+    slot->regen_base = std::min<uint64_t>(C, P * p.spp);
+    slot->ticket = ws.next_ticket++;
+    slot->pending = true;
+    *ticket_out = slot->ticket;
     return SPT_OK;
+}
+
+spt_status spt_render_wait(spt_scene sc, uint64_t ticket, spt_render_stats* stats_out) {
+    if (!sc) return fail(SPT_ERR_INVALID, "spt_render_wait: NULL scene");
+    std::lock_guard<std::mutex> lock(sc->mu);
+    RenderSlot& r = sc->ws.slots[ticket % kRenderSlots];
+    if (!r.pending || r.ticket != ticket)
+        return fail(SPT_ERR_INVALID, "spt_render_wait: ticket %llu is not a queued render (already collected, "
+                    "or %d renders were queued after it)", (unsigned long long)ticket, kRenderSlots);
+    return render_collect(r, stats_out);
+}
+
+spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev, spt_render_stats* stats_out,
+                      void* stream) {
+    uint64_t ticket = 0;
+    spt_status st = spt_render_async(sc, pp, film_dev, stream, &ticket);
+    if (st) return st;
+    return spt_render_wait(sc, ticket, stats_out);
 }
 
 }  // extern "C"

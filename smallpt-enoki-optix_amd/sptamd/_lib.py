@@ -29,7 +29,7 @@ SPT_BUILD_AUTO, SPT_BUILD_HOST_SAH, SPT_BUILD_GPU_PLOC = 0, 1, 2
 # Every function include/spt.h declares (the CPU test checks they are exported).
 EXPORTED = [
     "spt_init", "spt_scene_create", "spt_scene_create_ex", "spt_scene_set_albedo", "spt_scene_set_emission", "spt_scene_get_stats",
-    "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render",
+    "spt_scene_destroy", "spt_intersect", "spt_hit_info_compute", "spt_render", "spt_render_async", "spt_render_wait",
     "spt_tile_rows", "spt_default_params", "spt_last_error", "spt_version", "spt_build_id",
     "spt_obj_load", "spt_mesh_free", "spt_pfm_write", "spt_pbrt_load",
     "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
@@ -159,6 +159,8 @@ def _load() -> ctypes.CDLL:
         "spt_intersect": (i32, [vp, POINTER(Rays), vp, u32, POINTER(Hits), u32, i32, vp]),
         "spt_hit_info_compute": (i32, [vp, POINTER(Rays), POINTER(Hits), vp, u32, u32, POINTER(HitInfo), vp]),
         "spt_render": (i32, [vp, POINTER(RenderParams), vp, POINTER(RenderStats), vp]),
+        "spt_render_async": (i32, [vp, POINTER(RenderParams), vp, vp, POINTER(u64)]),
+        "spt_render_wait": (i32, [vp, u64, POINTER(RenderStats)]),
         "spt_tile_rows": (u32, [u32, u32, u32, u32, vp, u32]),
         "spt_default_params": (None, [POINTER(RenderParams)]),
         "spt_last_error": (c_char_p, []),

@@ -386,15 +386,35 @@ class Scene:
     def render(self, params: RenderParams, film: Optional[torch.Tensor] = None, stream=None):
         """One wavefront render of params' tile.  Returns (film (3, rows, W)
         float32 on the device, stats dict)."""
-        rows = _lib.tile_row_count(params.height, params.tile_index, params.tile_count, params.rows_per_group)
-        if film is None:
-            film = torch.empty((3, rows, params.width), dtype=torch.float32, device=self.backend.device)
-        assert film.is_contiguous() and film.numel() >= 3 * rows * params.width
+        film = self._film(params, film)
         st = RenderStats()
         self.backend.sync_config()
         check(lib.spt_render(self.backend.handle, ctypes.byref(params), film.data_ptr(), ctypes.byref(st),
                              _stream_handle(stream)), "spt_render")
         return film, st.as_dict()
+
+    def render_async(self, params: RenderParams, film: Optional[torch.Tensor] = None, stream=None):
+        """spt_render_async: queue the render and return (film, ticket) without
+        waiting for it; collect its stats with render_wait(ticket)."""
+        film = self._film(params, film)
+        ticket = ctypes.c_uint64()
+        self.backend.sync_config()
+        check(lib.spt_render_async(self.backend.handle, ctypes.byref(params), film.data_ptr(),
+                                   _stream_handle(stream), ctypes.byref(ticket)), "spt_render_async")
+        return film, ticket.value
+
+    def render_wait(self, ticket: int) -> dict:
+        """spt_render_wait: the stats dict of a queued render (waits for it)."""
+        st = RenderStats()
+        check(lib.spt_render_wait(self.backend.handle, ticket, ctypes.byref(st)), "spt_render_wait")
+        return st.as_dict()
+
+    def _film(self, params: RenderParams, film: Optional[torch.Tensor]) -> torch.Tensor:
+        rows = _lib.tile_row_count(params.height, params.tile_index, params.tile_count, params.rows_per_group)
+        if film is None:
+            film = torch.empty((3, rows, params.width), dtype=torch.float32, device=self.backend.device)
+        assert film.is_contiguous() and film.numel() >= 3 * rows * params.width
+        return film
 
 
 def scene_cache_info(path: str) -> dict:

@@ -280,3 +280,41 @@ def test_scheduling_knobs_invariance(gscene, oscene, monkeypatch, env):
     ref, casts = oracle_render(oscene, 48, 40, 7, 4)
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts
+
+
+def test_render_async_queue(gscene, oscene):
+    """spt_render_async / spt_render_wait: renders queued back to back (both
+    pipelines, different sizes, into different films) give the same images and
+    work accounting as the synchronous call, in any collection order; a ticket
+    is collected once; an empty tile queues nothing."""
+    jobs = [(48, 40, 7, 4, "wavefront"), (32, 24, 4, 3, "fused"), (40, 40, 5, 2, "wavefront")]
+    queued = []
+    for w, h, spp, depth, pipe in jobs:
+        film, ticket = gscene.render_async(sptamd.make_params(w, h, spp, depth, pipeline=pipe))
+        queued.append((film, ticket))
+    for (w, h, spp, depth, pipe), (film, ticket) in reversed(list(zip(jobs, queued))):
+        st = gscene.render_wait(ticket)
+        assert_work_complete(st, h, w, spp)
+        assert st["fused"] == (pipe == "fused")
+        ref, casts = oracle_render(oscene, w, h, spp, depth)
+        np.testing.assert_array_equal(film.cpu().numpy(), ref)
+        assert st["ray_casts"] == casts
+        with pytest.raises(sptamd.SptError):
+            gscene.render_wait(ticket)
+    # an empty tile (tile 5 of 6 with 8-row groups of a 16-row image)
+    _, t = gscene.render_async(sptamd.make_params(16, 16, 2, 2, tile_index=5, tile_count=6, rows_per_group=8))
+    st = gscene.render_wait(t)
+    assert st["tile_rows"] == 0 and st["paths"] == 0
+
+
+def test_render_async_limit(gscene):
+    """At most 64 renders queued without being collected: the 65th is refused
+    (SPT_ERR_LIMIT) and nothing is lost — every queued one still collects."""
+    p = sptamd.make_params(8, 8, 1, 1)
+    film = torch.empty((3, 8, 8), dtype=torch.float32, device="cuda")
+    tickets = [gscene.render_async(p, film=film)[1] for _ in range(64)]
+    with pytest.raises(sptamd.SptError) as e:
+        gscene.render_async(p, film=film)
+    assert e.value.code == sptamd._lib.SPT_ERR_LIMIT
+    for t in tickets:
+        assert gscene.render_wait(t)["paths"] == 64
