@@ -1360,10 +1360,26 @@ __global__ __launch_bounds__(256) void resolve_flags_kernel(const uint8_t* __res
     const uint32_t p = blockIdx.x * 256 + threadIdx.x;
     if (p >= P) return;
     uint32_t k = 0, lost = 0;
-    for (uint32_t s = 0; s < nsamples; s++) {
-        const uint32_t f = sflag[film_slot(s, p, P, nsamples, order)];
-        lost += f == kFlagSentinel ? 1u : 0u;
-        k += f & 1u;
+    if (order && nsamples % 16u == 0u) {
+        // pixel-major: this pixel's flags are nsamples contiguous bytes (16-B
+        // aligned), read 16 at a time; a flag byte is 0, 1 or the sentinel
+        // 0xff, so bit 7 counts the sentinels and bit 0 the escapes plus them
+        const uint4* f4 = reinterpret_cast<const uint4*>(sflag + (size_t)p * nsamples);
+        for (uint32_t c = 0; c < nsamples / 16u; c++) {
+            const uint4 w = f4[c];
+            const uint32_t hi = __popc(w.x & 0x80808080u) + __popc(w.y & 0x80808080u) + __popc(w.z & 0x80808080u) +
+                                __popc(w.w & 0x80808080u);
+            const uint32_t lo = __popc(w.x & 0x01010101u) + __popc(w.y & 0x01010101u) + __popc(w.z & 0x01010101u) +
+                                __popc(w.w & 0x01010101u);
+            lost += hi;
+            k += lo - hi;
+        }
+    } else {
+        for (uint32_t s = 0; s < nsamples; s++) {
+            const uint32_t f = sflag[film_slot(s, p, P, nsamples, order)];
+            lost += f == kFlagSentinel ? 1u : 0u;
+            k += f == 1u ? 1u : 0u;
+        }
     }
     if (lost) atomicAdd(unwritten, (unsigned long long)lost);
     const float env[3] = {env_r, env_g, env_b};
