@@ -269,22 +269,36 @@ def main():
                                f"expected {want} paths")
         return want
 
-    # gather timing events, created once (recorded on the render stream)
+    # gather timing events, created once (recorded on the step's stream)
     gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(max(args.steps, 1))]
+    # Consecutive steps alternate between two streams and two film buffers
+    # (the library alternates two working sets), so a step's render can start
+    # while the previous one drains; the gathers stay in step order.
+    streams = [stream, torch.cuda.Stream(device=dev)]
+    films = [film, tg.tile_view(1)]
+    last_gather = [None]
 
-    def step(p, i=None):
+    def step(p, i=None, k=0):
         """One step: the render of this rank's tile, queued (spt_render_async:
         the GPU runs from one step's render into the next without waiting for
-        the host), then the tile gather on the same stream.  Returns the
-        render's ticket; its device counters are collected after the loop."""
-        _, ticket = scene.render_async(p, film=film, stream=stream)
-        if i is not None:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
-            gev[i][0].record(stream)
-        tg.gather()
-        if i is not None:
-            gev[i][1].record(stream)
-            gather_ev.append(gev[i])
+        the host), then the tile gather behind it on the same stream, after the
+        previous step's gather.  Returns the render's ticket; its device
+        counters are collected after the loop."""
+        s = streams[k % 2]
+        with torch.cuda.stream(s):
+            _, ticket = scene.render_async(p, film=films[k % 2], stream=s)
+            if last_gather[0] is not None:
+                s.wait_event(last_gather[0])
+            if i is not None:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
+                gev[i][0].record(s)
+            tg.gather(k % 2)
+            done = torch.cuda.Event()
+            done.record(s)
+            last_gather[0] = done
+            if i is not None:
+                gev[i][1].record(s)
+                gather_ev.append(gev[i])
         return ticket
 
     def timed_loop(p, evs):
@@ -292,8 +306,8 @@ def main():
         synchronize; returns (max-over-ranks seconds, summed stats, last stats,
         device-counted paths of all ranks).  Every step's work accounting is
         checked once the timed region has ended."""
-        for _ in range(args.warmup):
-            check_work(scene.render_wait(step(p)))
+        for w in range(args.warmup):
+            check_work(scene.render_wait(step(p, k=w)))
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -302,7 +316,7 @@ def main():
         t0 = time.perf_counter()
         tickets, sts = [], []
         for i in range(args.steps):
-            tickets.append(step(p, i))
+            tickets.append(step(p, i, k=i))
             if len(tickets) > 32:  # the library holds at most 64 uncollected renders
                 sts.append(scene.render_wait(tickets.pop(0)))
         torch.cuda.synchronize()

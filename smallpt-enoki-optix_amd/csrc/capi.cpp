@@ -128,16 +128,20 @@ struct Sub {
     hipEvent_t join_ev = nullptr;
 };
 
-struct Workspace {
+// One render's working memory: path queues, counters and sub-wavefront
+// streams, the per-sample film chunk and the running sum.  A scene keeps two
+// (kWorkSets), used by alternate renders, so a render queued on another stream
+// can start while the previous one drains; a render waits for the last render
+// that used its set (free_ev), so any stream use stays race-free.
+constexpr int kWorkSets = 2;
+struct WorkSet {
     Sub sub[kMaxStreams];
-    size_t film_cap = 0, acc_cap = 0, jump_cap = 0;
+    size_t film_cap = 0, acc_cap = 0;
     char* film = nullptr;               // per-sample contributions of a chunk (bytes or RGB floats)
     float* acc = nullptr;               // [3][P] running sum across chunks
-    PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps
-    uint32_t jump_key_spp = 0, jump_key_depth = 0;
-    RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
-    uint64_t next_ticket = 1;
     hipEvent_t fork_ev = nullptr;
+    hipEvent_t free_ev = nullptr;       // recorded on the stream of the last render that used the set
+    bool used = false;                  // free_ev has been recorded
 
     void release() {
         for (Sub& b : sub) {
@@ -147,14 +151,30 @@ struct Workspace {
             if (b.join_ev) (void)hipEventDestroy(b.join_ev);
             if (b.stream) (void)hipStreamDestroy(b.stream);
         }
-        hfree(film); hfree(acc); hfree(jumps);
+        hfree(film); hfree(acc);
+        if (fork_ev) (void)hipEventDestroy(fork_ev);
+        if (free_ev) (void)hipEventDestroy(free_ev);
+        *this = WorkSet();
+    }
+};
+
+struct Workspace {
+    WorkSet sets[kWorkSets];
+    size_t jump_cap = 0;
+    PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps (read-only)
+    uint32_t jump_key_spp = 0, jump_key_depth = 0;
+    RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
+    uint64_t next_ticket = 1;
+
+    void release() {
+        for (WorkSet& w : sets) w.release();
+        hfree(jumps);
         for (RenderSlot& r : slots) {
             hfree(r.dev);
             if (r.host) (void)hipHostFree(r.host);
             for (auto e : r.events) (void)hipEventDestroy(e);
             if (r.done) (void)hipEventDestroy(r.done);
         }
-        if (fork_ev) (void)hipEventDestroy(fork_ev);
         const uint64_t t = next_ticket;  // tickets stay unique over the scene's life
         *this = Workspace();
         next_ticket = t;
@@ -257,11 +277,21 @@ Camera make_camera(const spt_render_params& p) {
     return cam;
 }
 
-spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, uint32_t planes, size_t film_bytes,
-                            size_t acc_floats, size_t njumps) {
+// A set's buffers for this render; a buffer that must grow is freed only after
+// the last render that used the set has finished with it.
+spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uint32_t planes, size_t film_bytes,
+                            size_t acc_floats) {
+    bool quiet = !ws.used;
+    const auto quiesce = [&]() -> spt_status {
+        if (!quiet) HIP_TRY(hipEventSynchronize(ws.free_ev));
+        quiet = true;
+        return SPT_OK;
+    };
+    spt_status st;
     for (int k = 0; k < nsub; k++) {
         Sub& b = ws.sub[k];
         if (cap > b.cap || pad != b.pad || planes > b.planes) {
+            if ((st = quiesce())) return st;
             hfree(b.qa); hfree(b.qb); hfree(b.hits);
             b.cap = 0;
             HIP_TRY(hipMalloc((void**)&b.qa, (size_t)16 * planes * queue_stride(cap, pad)));
@@ -279,25 +309,45 @@ spt_status ensure_workspace(Workspace& ws, int nsub, size_t cap, uint32_t pad, u
         if (k > 0 && !b.stream) HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
     }
     if (film_bytes > ws.film_cap) {
+        if ((st = quiesce())) return st;
         hfree(ws.film);
         ws.film_cap = 0;
         HIP_TRY(hipMalloc((void**)&ws.film, film_bytes));
         ws.film_cap = film_bytes;
     }
     if (acc_floats > ws.acc_cap) {
+        if ((st = quiesce())) return st;
         hfree(ws.acc);
         ws.acc_cap = 0;
         HIP_TRY(hipMalloc((void**)&ws.acc, sizeof(float) * acc_floats));
         ws.acc_cap = acc_floats;
     }
-    if (njumps > ws.jump_cap) {
-        hfree(ws.jumps);
-        ws.jump_cap = 0;
-        ws.jump_key_spp = 0;
-        HIP_TRY(hipMalloc((void**)&ws.jumps, sizeof(PcgJump) * njumps));
-        ws.jump_cap = njumps;
-    }
     if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
+    if (!ws.free_ev) HIP_TRY(hipEventCreateWithFlags(&ws.free_ev, hipEventDisableTiming));
+    return SPT_OK;
+}
+
+// The PCG32 jump table (shared by the sets, read-only while renders run): to
+// each sample's first draw, s * (4 + 2D), and from there to the bounce draw
+// of each cast, 4 + 2 * cast (main.cpp:395,396,413).  Rewritten only when
+// spp or depth change, after every queued render has finished with it.
+spt_status ensure_jumps(Workspace& w, uint32_t spp, uint32_t depth) {
+    if (w.jumps && w.jump_key_spp == spp && w.jump_key_depth == depth) return SPT_OK;
+    if (w.jumps) HIP_TRY(hipDeviceSynchronize());
+    const size_t n = (size_t)spp + kMaxDepthCasts;
+    if (n > w.jump_cap) {
+        hfree(w.jumps);
+        w.jump_cap = 0;
+        HIP_TRY(hipMalloc((void**)&w.jumps, sizeof(PcgJump) * n));
+        w.jump_cap = n;
+    }
+    const uint64_t per_sample = 4ull + 2ull * depth;
+    std::vector<PcgJump> jt((size_t)spp + depth);
+    for (uint32_t s = 0; s < spp; s++) jt[s] = pcg_jump_coeffs((uint64_t)s * per_sample);
+    for (uint32_t j = 0; j < depth; j++) jt[(size_t)spp + j] = pcg_jump_coeffs(4ull + 2ull * j);
+    HIP_TRY(hipMemcpy(w.jumps, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
+    w.jump_key_spp = spp;
+    w.jump_key_depth = depth;
     return SPT_OK;
 }
 
@@ -1622,26 +1672,16 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
     rs.paths_in_flight = (uint32_t)C;
-    st = ensure_workspace(sc->ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P,
-                                     3 * P, (size_t)p.spp + kMaxDepthCasts);
+    WorkSet& ws = sc->ws.sets[sc->ws.next_ticket % kWorkSets];
+    st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P);
     if (st) return st;
-    Workspace& ws = sc->ws;
+    if ((st = ensure_jumps(sc->ws, p.spp, p.max_depth))) return st;
+    const PcgJump* jumps = sc->ws.jumps;
     // HIP events around the isect launches (the roofline kernel); every other
     // launch only with SPT_FLAG_TIMING_ALL (each event pair costs host time).
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
     const bool timing_all = timing && (p.flags & SPT_FLAG_TIMING_ALL) != 0;
 
-    // PCG32 jump to each sample's first draw, s * (4 + 2D), and from there to
-    // the bounce draw of each cast, 4 + 2 * cast (main.cpp:395,396,413).
-    const uint64_t per_sample = 4ull + 2ull * p.max_depth;
-    if (ws.jump_key_spp != p.spp || ws.jump_key_depth != p.max_depth) {
-        std::vector<PcgJump> jt((size_t)p.spp + p.max_depth);
-        for (uint32_t s = 0; s < p.spp; s++) jt[s] = pcg_jump_coeffs((uint64_t)s * per_sample);
-        for (uint32_t j = 0; j < p.max_depth; j++) jt[(size_t)p.spp + j] = pcg_jump_coeffs(4ull + 2ull * j);
-        HIP_TRY(hipMemcpy(ws.jumps, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
-        ws.jump_key_spp = p.spp;
-        ws.jump_key_depth = p.max_depth;
-    }
 
     const Camera cam = make_camera(p);
     float* sfilm = (float*)ws.film;
@@ -1663,6 +1703,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     };
     hipStream_t strm[kMaxStreams];
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
+    // the set's previous render (another stream, perhaps) must be done with it
+    if (ws.used) HIP_TRY(hipStreamWaitEvent(stream, ws.free_ev, 0));
     HIP_TRY(hipMemsetAsync(slot->dev, 0, sizeof(Stats), stream));
     // time origin for the isect launch intervals (their union = isect busy time)
     slot->timing = timing;
@@ -1719,8 +1761,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         S.hits = (const float4*)b.hits;
         S.sfilm = sfilm;
         S.sflag = sflag;
-        S.sample_jump = ws.jumps;
-        S.cast_jump = ws.jumps + p.spp;
+        S.sample_jump = jumps;
+        S.cast_jump = jumps + p.spp;
         S.initstate = p.rng_initstate;
         S.P = (uint32_t)P; S.W = p.width; S.max_depth = p.max_depth;
         S.xcd_remap = (cfg.xcd_remap >> 1) & 1u;
@@ -1730,7 +1772,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];
         RefillArgs& R = ra[k];
         R.cam = cam;
-        R.sample_jump = ws.jumps;
+        R.sample_jump = jumps;
         R.stats = slot->dev->stats;
         R.capacity = (uint32_t)b.cap; R.P = (uint32_t)P; R.W = p.width; R.rng_order = p.rng_order;
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
@@ -1746,7 +1788,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         FusedArgs F;
         F.sc = sc->dev();
         F.cam = cam;
-        F.sample_jump = ws.jumps;
+        F.sample_jump = jumps;
         F.sfilm = sfilm;
         F.sflag = sflag;
         F.stats = slot->dev->stats;
@@ -1921,12 +1963,14 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // pinned destination: a pageable one makes the copy a staged, slower transfer
     HIP_TRY(hipMemcpyAsync(slot->host, slot->dev, sizeof(Stats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipEventRecord(slot->done, stream));
+    HIP_TRY(hipEventRecord(ws.free_ev, stream));  // every sub-stream joined `stream` before the resolve
+    ws.used = true;
     rs.iterations = iters;
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
     rs.streams = (uint32_t)K;
     rs.fused = fused ? 1u : 0u;
     slot->regen_base = std::min<uint64_t>(C, P * p.spp);
-    slot->ticket = ws.next_ticket++;
+    slot->ticket = sc->ws.next_ticket++;
     slot->pending = true;
     *ticket_out = slot->ticket;
     return SPT_OK;

@@ -24,8 +24,11 @@ class TileGather:
         self.rows: List = [tile_rows(height, r, world, rows_per_group) for r in range(world)]
         self.max_rows = max(1, max(len(r) for r in self.rows))
         self.device = device
-        # flat so that every rank's (3, rows, W) film is one contiguous prefix
-        self.tile = torch.zeros(3 * self.max_rows * width, dtype=torch.float32, device=device)
+        # flat so that every rank's (3, rows, W) film is one contiguous prefix;
+        # two of them, so that consecutive steps can render on two streams
+        # while the previous step's tile is still being gathered
+        self.tiles = [torch.zeros(3 * self.max_rows * width, dtype=torch.float32, device=device)]
+        self.tile = self.tiles[0]
         self.gather_list: Optional[List[torch.Tensor]] = None
         self.image: Optional[torch.Tensor] = None
         if rank == 0:
@@ -38,25 +41,29 @@ class TileGather:
     def my_rows(self) -> int:
         return len(self.rows[self.rank])
 
-    def tile_view(self) -> torch.Tensor:
-        """The (3, my_rows, W) film buffer spt_render writes into."""
-        return self.tile[: 3 * self.my_rows * self.W].view(3, self.my_rows, self.W)
+    def tile_view(self, k: int = 0) -> torch.Tensor:
+        """The (3, my_rows, W) film buffer k (0 or 1) spt_render writes into."""
+        while len(self.tiles) <= k:
+            self.tiles.append(torch.zeros_like(self.tiles[0]))
+        return self.tiles[k][: 3 * self.my_rows * self.W].view(3, self.my_rows, self.W)
 
-    def gather(self) -> Optional[torch.Tensor]:
-        """Collective: every rank calls it; rank 0 gets the assembled image."""
+    def gather(self, k: int = 0) -> Optional[torch.Tensor]:
+        """Collective: every rank calls it; rank 0 gets the assembled image
+        from every rank's film buffer k (on the current stream)."""
+        tile = self.tiles[k]
         if self.world == 1:
-            self.image.copy_(self.tile_view())
+            self.image.copy_(self.tile_view(k))
             return self.image
-        if self.tile.is_cuda and dist.get_backend() != "nccl":
+        if tile.is_cuda and dist.get_backend() != "nccl":
             # gloo gathers host tensors only (the CPU rehearsal of the N-rank flow)
-            tile = self.tile.cpu()
+            tile = tile.cpu()
             glist = [torch.empty_like(tile) for _ in range(self.world)] if self.rank == 0 else None
             dist.gather(tile, glist, dst=0)
             if self.rank == 0:
                 for r in range(self.world):
                     self.gather_list[r].copy_(glist[r])
         else:
-            dist.gather(self.tile, self.gather_list if self.rank == 0 else None, dst=0)
+            dist.gather(tile, self.gather_list if self.rank == 0 else None, dst=0)
         if self.rank != 0:
             return None
         for r in range(self.world):

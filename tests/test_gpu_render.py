@@ -318,3 +318,24 @@ def test_render_async_limit(gscene):
     assert e.value.code == sptamd._lib.SPT_ERR_LIMIT
     for t in tickets:
         assert gscene.render_wait(t)["paths"] == 64
+
+
+def test_render_async_two_streams(gscene, oscene):
+    """Renders queued on alternating streams use alternating working sets and
+    may overlap on the GPU; each waits for the last render of its set, so
+    back-to-back renders of different sizes and pipelines on two streams give
+    the oracle's images bit for bit."""
+    jobs = [(48, 40, 7, 4, "wavefront"), (32, 24, 4, 3, "fused"), (40, 40, 5, 2, "fused"), (24, 20, 2, 8, "wavefront"),
+            (33, 17, 3, 1, "fused")]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    queued = []
+    for i, (w, h, spp, depth, pipe) in enumerate(jobs):
+        film, ticket = gscene.render_async(sptamd.make_params(w, h, spp, depth, pipeline=pipe),
+                                           stream=streams[(i // 2) % 2])  # sets and streams out of phase
+        queued.append((film, ticket))
+    torch.cuda.synchronize()
+    for (w, h, spp, depth, pipe), (film, ticket) in zip(jobs, queued):
+        st = gscene.render_wait(ticket)
+        assert_work_complete(st, h, w, spp)
+        ref, _ = oracle_render(oscene, w, h, spp, depth)
+        np.testing.assert_array_equal(film.cpu().numpy(), ref)

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--pipeline", default=None, help="wavefront | fused (default: the library's auto choice)")
     ap.add_argument("--timing", action="store_true", help="HIP events around every launch (as bench.py)")
     ap.add_argument("--wavefront", type=int, default=0, help="paths in flight (0 = the library default)")
+    ap.add_argument("--sync", action="store_true", help="spt_render per step (no queued renders)")
     args = ap.parse_args()
     import torch
 
@@ -52,14 +53,20 @@ def main():
                                timing=args.timing, pipeline=args.pipeline,
                                wavefront_paths=args.wavefront, **kw)
         rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
-        film = torch.empty((3, rows, W), dtype=torch.float32, device="cuda")
-        scene.render(p, film=film)
+        films = [torch.empty((3, rows, W), dtype=torch.float32, device="cuda") for _ in range(2)]
+        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        scene.render(p, film=films[0])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            _, st = scene.render(p, film=film)
+        if args.sync:
+            for _ in range(args.steps):
+                _, st = scene.render(p, film=films[0])
+        else:  # as bench.py: renders queued back to back on two alternating streams
+            tickets = [scene.render_async(p, film=films[i % 2], stream=streams[i % 2])[1] for i in range(args.steps)]
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
+        if not args.sync:
+            st = [scene.render_wait(t) for t in tickets][-1]
         paths = rows * W * spp
         rate = paths / dt / 1e6
         print(json.dumps({"tiles": n, "tile_rows": rows, "ms_per_step": round(dt * 1e3, 3),
