@@ -331,6 +331,11 @@ def main():
             check_work(st)
             for k in agg:
                 agg[k] += st[k]
+        # consecutive renders overlap on the GPU (two streams, two working
+        # sets): the kernel's busy time is the union over the renders, each
+        # render's own union less its overlap with the next (on one clock)
+        for a_, b_ in zip(sts, sts[1:]):
+            agg["isect_busy_ms"] -= max(0.0, min(a_["isect_end_ms"], b_["isect_end_ms"]) - b_["isect_begin_ms"])
         tot = [agg["ray_casts"], agg["continuations"], agg["paths"]]
         if world > 1:
             rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
@@ -464,6 +469,8 @@ def main():
                          "traffic_per_unit": traffic_per_unit,
                          "traffic_ratio": round(traffic / bytes_per_launch, 3) if traffic else None,
                          "busy_ms_per_step": round(busy_ms / args.steps, 4),
+                         "busy_note": "union over the step's launch intervals and over consecutive steps' renders, "
+                                      "which overlap on two streams",
                          "launches_per_step": round(launches / args.steps, 2),
                          "avg_launch_ms": round(avg_ms, 4),
                          "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None,

@@ -137,6 +137,10 @@ typedef struct spt_render_stats {
     uint32_t reserved0;
     uint64_t isect_tri_wave_steps;  /* SPT_FLAG_TRAVERSAL_STATS: wave steps in which some lane tested a triangle */
     uint64_t isect_node_wave_steps; /*   ... in which some lane visited a node */
+    double isect_begin_ms, isect_end_ms; /* SPT_FLAG_TIMING: start of the first / end of the last isect launch
+                                            (the fused kernel's launches in the fused pipeline), in ms from one
+                                            clock per scene (the first timed render): renders queued back to
+                                            back may overlap, and their union is the kernel's busy time */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {

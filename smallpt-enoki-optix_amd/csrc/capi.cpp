@@ -165,9 +165,11 @@ struct Workspace {
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
     RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
     uint64_t next_ticket = 1;
+    hipEvent_t epoch = nullptr;         // the first timed render's time origin: isect_begin/end_ms count from it
 
     void release() {
         for (WorkSet& w : sets) w.release();
+        if (epoch) (void)hipEventDestroy(epoch);
         hfree(jumps);
         for (RenderSlot& r : slots) {
             hfree(r.dev);
@@ -379,7 +381,7 @@ spt_status render_slot(Workspace& ws, RenderSlot** out) {
 
 // Waits for a queued render and fills its statistics (device counters, the
 // union of its isect launch intervals, host wall time since it was queued).
-spt_status render_collect(RenderSlot& r, spt_render_stats* out) {
+spt_status render_collect(RenderSlot& r, hipEvent_t epoch, spt_render_stats* out) {
     spt_render_stats rs = r.rs;
     r.pending = false;
     if (rs.tile_rows) {  // an empty tile queued nothing
@@ -419,6 +421,14 @@ spt_status render_collect(RenderSlot& r, spt_render_stats* out) {
             rs.isect_launches = nis;
             // launches on the K streams overlap: busy time = union of their intervals
             std::sort(iv.begin(), iv.end());
+            if (!iv.empty() && epoch) {  // the span on the scene's clock, for unions across queued renders
+                float t_origin = 0.0f;
+                HIP_TRY(hipEventElapsedTime(&t_origin, epoch, r.events[0]));
+                float last = iv[0].second;
+                for (auto& x : iv) last = std::max(last, x.second);
+                rs.isect_begin_ms = (double)t_origin + iv[0].first;
+                rs.isect_end_ms = (double)t_origin + last;
+            }
             float lo = 0.0f, hi = -1.0f;
             for (auto& x : iv) {
                 if (x.first > hi) {
@@ -1711,6 +1721,10 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     if (timing) {
         hipEvent_t origin_ev = nullptr;
         if ((st = get_event(*slot, 0, &origin_ev))) return st;
+        if (!sc->ws.epoch) {
+            HIP_TRY(hipEventCreate(&sc->ws.epoch));
+            HIP_TRY(hipEventRecord(sc->ws.epoch, stream));
+        }
         HIP_TRY(hipEventRecord(origin_ev, stream));
     }
 
@@ -1983,7 +1997,7 @@ spt_status spt_render_wait(spt_scene sc, uint64_t ticket, spt_render_stats* stat
     if (!r.pending || r.ticket != ticket)
         return fail(SPT_ERR_INVALID, "spt_render_wait: ticket %llu is not a queued render (already collected, "
                     "or %d renders were queued after it)", (unsigned long long)ticket, kRenderSlots);
-    return render_collect(r, stats_out);
+    return render_collect(r, sc->ws.epoch, stats_out);
 }
 
 spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev, spt_render_stats* stats_out,

@@ -89,7 +89,8 @@ class RenderStats(ctypes.Structure):
                 ("isect_max_stack", c_uint64),
                 ("paths_started", c_uint64), ("paths_terminated", c_uint64), ("film_slots_unwritten", c_uint64),
                 ("work_order", c_uint32), ("reserved0", c_uint32),
-                ("isect_tri_wave_steps", c_uint64), ("isect_node_wave_steps", c_uint64)]
+                ("isect_tri_wave_steps", c_uint64), ("isect_node_wave_steps", c_uint64),
+                ("isect_begin_ms", c_double), ("isect_end_ms", c_double)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_}
