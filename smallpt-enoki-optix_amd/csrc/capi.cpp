@@ -75,12 +75,17 @@ PathQueue carve_queue(char* base, size_t stride, uint32_t planes) {
 size_t queue_stride(size_t cap, uint32_t pad) { return cap + pad; }
 
 // Device counters of one sub-wavefront (zeroed per chunk; see spt_render).
+// The atomically updated counters sit in 128-B lines of their own: a line that
+// takes atomics (shade blocks' survivor counts, isect waves' work grabs) slows
+// every plain load of the same line from the other waves (config 1 +1.2 %;
+// EXPERIMENTS.md, r3_counter_lines).
 struct Counters {
     uint32_t qn[2];      // queue counts (isect/shade input)
-    uint32_t surv[2];    // survivors appended by shade
+    alignas(128) uint32_t surv[2];    // survivors appended by shade
     uint64_t cursor[2];  // next work item (double-buffered across refills)
-    uint32_t isect_next; // persistent isect work counter (zeroed by each refill)
-    uint32_t pad[3];
+    alignas(128) uint32_t isect_next; // persistent isect work counter (zeroed by each refill)
+    uint32_t exhausted;  // RefillArgs::iter_tag of the refill that started the last work item (0: not yet)
+    uint32_t pad[2];
 };
 
 // Render-wide device statistics.
@@ -1795,6 +1800,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         R.initstate = p.rng_initstate;
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
+        R.exhausted = &b.cnt->exhausted;
     }
 
     uint64_t iters = 0;
@@ -1865,6 +1871,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];
             ra[k].surv_clear = nullptr;
             ra[k].casts_in = nullptr;
+            ra[k].iter_tag = 1;
             const uint32_t first = (uint32_t)std::min<uint64_t>(b.cap, we - wb);
             sub_begin[k] = wb;
             sub_end[k] = we;
@@ -1895,7 +1902,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             live[k] = known[k] > 0;
         }
         uint64_t it = 0;
-        uint32_t batch = 4, nbatch = 0;
+        const uint32_t batch = 4;
+        uint32_t nbatch = 0;
         int nlive = 0;
         for (int k = 0; k < K; k++) nlive += live[k] ? 1 : 0;
         while (nlive > 0) {
@@ -1925,6 +1933,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                     ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
                     ra[k].surv_clear = &b.cnt->surv[c];
                     ra[k].casts_in = &b.cnt->qn[c];
+                    ra[k].iter_tag = (uint32_t)it + 2;
                     // new paths: at most the work not yet known to be started (one
                     // block still runs to carry the counters over)
                     const uint32_t fill = (uint32_t)std::min<uint64_t>(b.cap, sub_end[k] - started[k]);
@@ -1955,7 +1964,10 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         nlive--;
                         continue;
                     }
-                    if (started[k] >= sub_end[k]) limit[k] = pend_it[k] + p.max_depth;
+                    // the refill after iteration T - 2 (tag T) started the last
+                    // work item: its paths cast in iterations T - 1 .. T + max_depth - 2
+                    if (hc.exhausted) limit[k] = hc.exhausted - 1 + p.max_depth;
+                    else if (started[k] >= sub_end[k]) limit[k] = pend_it[k] + p.max_depth;
                 }
                 pending[k] = slot;
                 pend_cur[k] = cur[k];
@@ -1964,7 +1976,9 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             if (it > max_iters)
                 return fail(SPT_ERR_HIP, "spt_render: queue did not drain after %llu iterations",
                             (unsigned long long)it);
-            batch = std::min<uint32_t>(batch * 2, 16);
+            // the batch stays short: the first readback that shows the last work
+            // item started bounds the loop, and a long batch would overshoot it
+            // (the GPU still has one batch queued while the host waits)
         }
         iters += it;
         // join the sub-wavefront streams back into the caller's stream

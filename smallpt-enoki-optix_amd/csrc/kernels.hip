@@ -924,6 +924,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         *a.qn_out = surv + total;
         *a.isect_next = 0;
         if (a.surv_clear) *a.surv_clear = 0;
+        if (cur < a.work_end && cur + total >= a.work_end) *a.exhausted = a.iter_tag;
         if (a.casts_in) {  // the shade before: its queue count and its survivors
             const uint32_t casts = *a.casts_in;
             if (casts) atomicAdd(&a.stats[0], (unsigned long long)casts);

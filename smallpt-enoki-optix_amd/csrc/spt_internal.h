@@ -280,6 +280,8 @@ struct RefillArgs {
                                 // thread 0 adds it and *surv to stats[0] / stats[1]
     const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
     unsigned long long* stats;  // casts, continuations, regenerations
+    uint32_t* exhausted;        // thread 0 writes iter_tag here when this refill starts the last work item
+    uint32_t iter_tag;          // the host's iteration number + 2 (the chunk's first refill: 1)
     uint64_t work_end;          // W_total (work items of this chunk end here)
     uint32_t capacity, P, W, rng_order;
     uint32_t tile_index, tile_count, rows_per_group;
