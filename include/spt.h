@@ -243,7 +243,10 @@ typedef struct spt_config {
     uint32_t public_refill_idle;    /* its refill threshold, 16                              [1..64] */
     /* --- scene build, continued */
     uint32_t pack_groups;           /* 1: wide-BVH child groups packed into each other's empty
-                                       slots (denser node lines), 0: eight aligned slots each [0..1] */
+                                       slots (denser node lines) in build order (level by level
+                                       for the GPU builder), 2: packed in depth-first order (a
+                                       subtree's groups near each other), 0: eight aligned slots
+                                       each [0..2] */
     /* --- spt_render, continued */
     uint32_t pixel_block;           /* camera paths start in B x B pixel blocks, 0 (0 or 1:
                                        scanline, measured fastest: DESIGN.md §4); the image

@@ -489,7 +489,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(film_budget_bytes, 12, UINT64_MAX)
     CFG_RANGE(public_persistent, 0, 1)
     CFG_RANGE(public_refill_idle, 1, 64)
-    CFG_RANGE(pack_groups, 0, 1)
+    CFG_RANGE(pack_groups, 0, 2)
     CFG_RANGE(pixel_block, 0, 64)
     CFG_RANGE(work_order, 0, SPT_WORK_PIXEL_MAJOR)
 #undef CFG_RANGE
@@ -533,7 +533,7 @@ spt_status create_scene_gpu(const int32_t* pos_tri, const float* pos, uint64_t n
     {
         uint32_t* holes = nullptr;
         const hipError_t he = gpu_bvh8_holes(g.nodes8, g.nnodes, s, &holes, &nslots, width,
-                                             cfg.pack_groups ? &sc->group_shift : nullptr);
+                                             cfg.pack_groups ? &sc->group_shift : nullptr, cfg.pack_groups == 2);
         (void)hipFree(g.nodes8);
         if (he) {
             (void)hipFree(g.slot2tri);
@@ -777,7 +777,7 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
         if (!us) {
             uint32_t* holes = nullptr;
             const hipError_t he = gpu_bvh8_holes(compact, (uint32_t)nn, nullptr, &holes, &nslots, width,
-                                                 cfg.pack_groups ? &sc->group_shift : nullptr);
+                                                 cfg.pack_groups ? &sc->group_shift : nullptr, cfg.pack_groups == 2);
             if (he) us = fail(he == hipErrorOutOfMemory ? SPT_ERR_OOM : SPT_ERR_HIP,
                               "spt_scene_create (BVH8 layout): %s", hipGetErrorString(he));
             else {

@@ -38,9 +38,12 @@ hipError_t gpu_build_bvh8(const float* d_tv, uint32_t ntri, hipStream_t s, GpuBv
 // into each other's holes (a node's group word is its first child slot,
 // *group_shift = 0) when that fits 24 bits, else aligned (group word = slot /
 // 8, *group_shift = 3); null: aligned.  Child s of a node sits at
-// (group word << shift) + s.
+// (group word << shift) + s.  depth_first: the groups are packed in the
+// order a depth-first walk from the root meets them (children in slot order)
+// instead of build order, so a subtree's groups lie near each other.
 hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t nnodes, hipStream_t s, uint32_t** out,
-                          uint32_t* nslots, int width = 8, uint32_t* group_shift = nullptr);
+                          uint32_t* nslots, int width = 8, uint32_t* group_shift = nullptr,
+                          bool depth_first = false);
 
 }  // namespace spt
 

@@ -674,8 +674,38 @@ static size_t pack_groups(const std::vector<uint8_t>& gmask, std::vector<uint32_
     return end;
 }
 
+// Group ids in depth-first order from the root: group g holds the inner
+// children of the g-th node (in node order) that has any; a node's inner
+// children are nodes w4 .. w4 + popcount(imask) - 1 (compact layout).
+static std::vector<uint32_t> depth_first_groups(const std::vector<uint32_t>& w34, uint32_t n, uint32_t groups) {
+    std::vector<uint32_t> gid(n, UINT32_MAX);
+    for (uint32_t i = 0, g = 0; i < n; i++)
+        if (w34[2 * i] >> 24) gid[i] = g++;
+    std::vector<uint32_t> order;
+    order.reserve(groups);
+    std::vector<uint32_t> stack{0u};
+    while (!stack.empty()) {
+        const uint32_t i = stack.back();
+        stack.pop_back();
+        const uint32_t imask = w34[2 * i] >> 24;
+        if (!imask || i >= n) continue;
+        order.push_back(gid[i]);
+        const uint32_t first = w34[2 * i + 1], cnt = (uint32_t)__builtin_popcount(imask);
+        for (uint32_t c = cnt; c-- > 0;)  // first child on top: visited first
+            if (first + c < n) stack.push_back(first + c);
+    }
+    // groups the walk did not reach (none in a well-formed tree) keep build order
+    if (order.size() != groups) {
+        std::vector<uint8_t> seen(groups, 0);
+        for (uint32_t g : order) seen[g] = 1;
+        for (uint32_t g = 0; g < groups; g++)
+            if (!seen[g]) order.push_back(g);
+    }
+    return order;
+}
+
 hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, uint32_t** out, uint32_t* nslots,
-                          int width, uint32_t* group_shift) {
+                          int width, uint32_t* group_shift, bool depth_first) {
     *out = nullptr;
     *nslots = 0;
     if (group_shift) *group_shift = 3;
@@ -714,7 +744,20 @@ hipError_t gpu_bvh8_holes(const uint32_t* d_nodes, uint32_t n, hipStream_t s, ui
         std::vector<uint8_t> hm(groups);
         GB_TRY(hipMemcpyAsync(hm.data(), gmask, groups, hipMemcpyDeviceToHost, s));
         GB_TRY(hipStreamSynchronize(s));
-        slots = pack_groups(hm, gw);
+        if (depth_first) {
+            // words 3 (inner mask) and 4 (first inner child) of every node
+            std::vector<uint32_t> w34(2 * (size_t)n);
+            GB_TRY(hipMemcpy2DAsync(w34.data(), 8, d_nodes + 3, kNode8Quads * 16, 8, n, hipMemcpyDeviceToHost, s));
+            GB_TRY(hipStreamSynchronize(s));
+            const std::vector<uint32_t> order = depth_first_groups(w34, n, groups);
+            std::vector<uint8_t> pm(groups);
+            for (uint32_t k = 0; k < groups; k++) pm[k] = hm[order[k]];
+            std::vector<uint32_t> pw;
+            slots = pack_groups(pm, pw);
+            for (uint32_t k = 0; k < groups && slots; k++) gw[order[k]] = pw[k];
+        } else {
+            slots = pack_groups(hm, gw);
+        }
         if (slots) shift = 0;
     }
     if (shift) {

@@ -68,7 +68,7 @@ def test_gpu_build_render_bitexact(mesh, pipeline):
     np.testing.assert_array_equal(h, ref)
 
 
-@pytest.mark.parametrize("pack,collapse", [(1, 0), (0, 0), (1, 1)])
+@pytest.mark.parametrize("pack,collapse", [(1, 0), (0, 0), (1, 1), (2, 0)])
 @pytest.mark.parametrize("width", [6, 8])
 @pytest.mark.parametrize("build", [HOST, GPU])
 def test_node_formats_bitexact(mesh, width, build, pack, collapse):

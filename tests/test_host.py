@@ -172,7 +172,7 @@ def test_config_defaults_and_env_overrides():
 
 @pytest.mark.parametrize("field,value", [("streams", 0), ("streams", 5), ("bvh_width", 4), ("ploc_radius", 12),
                                          ("isect_refill_idle", 65), ("film_budget_bytes", 0), ("pipeline", 3),
-                                         ("bvh_width", 7), ("pack_groups", 2)])
+                                         ("bvh_width", 7), ("pack_groups", 3)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)
