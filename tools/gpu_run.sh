@@ -48,6 +48,8 @@ for s in "$@"; do
     pmcshade) run pmcshade 600 env KERNEL=shade_kernel bash tools/pmc_sweep.sh gpurun_out/pmc_shade "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" ;;
     pmcshade1) run pmcshade1 600 env SPT_STREAMS=1 KERNEL=shade_kernel bash tools/pmc_sweep.sh gpurun_out/pmc_shade1 "FETCH_SIZE" "WRITE_SIZE" ;;
     pmc1s) run pmc1s 900 env SPT_STREAMS=1 CONFIG=1 bash tools/pmc_isect.sh gpurun_out/pmc1s ;;
+    proff) run proff 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proff -o run --output-format csv -- python bench.py --pipeline fused --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcf) run pmcf 900 env CONFIG=1 PIPE=fused bash tools/pmc_isect.sh gpurun_out/pmc ;;
     prof1s) run prof1s 600 env SPT_STREAMS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1s -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
     trav4) run trav4 600 python tools/trav_stats.py --city --depths 8 --spp 8 ;;
