@@ -269,7 +269,11 @@ def main():
                                f"expected {want} paths")
         return want
 
-    SETUP_RENDERS = 2  # the library's two working sets, the bench's two streams
+    # one setup render per stream: the library binds a working set to each
+    # caller stream (spt.h spt_render_async); SPT_BENCH_SETUP / SPT_BENCH_SYNC
+    # (experiment knobs, tools/ov.sh): setup renders, one render at a time
+    SETUP_RENDERS = int(os.environ.get("SPT_BENCH_SETUP", "2"))
+    SYNC_STEPS = os.environ.get("SPT_BENCH_SYNC", "0") == "1"
     # gather timing events, created once (recorded on the step's stream)
     gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(max(args.steps, 1))]
@@ -323,6 +327,8 @@ def main():
         tickets, sts = [], []
         for i in range(args.steps):
             tickets.append(step(p, i, k=i))
+            if SYNC_STEPS:
+                sts.append(scene.render_wait(tickets.pop(0)))
             if len(tickets) > 32:  # the library holds at most 64 uncollected renders
                 sts.append(scene.render_wait(tickets.pop(0)))
         torch.cuda.synchronize()

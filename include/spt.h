@@ -405,7 +405,10 @@ spt_status spt_render(spt_scene scene, const spt_render_params* params, float* f
  * fills its statistics (stats may be NULL); every ticket must be collected
  * once, and at most 64 renders of a scene may be queued without being
  * collected (SPT_ERR_LIMIT).  spt_render(...) = spt_render_async +
- * spt_render_wait. */
+ * spt_render_wait.  A scene keeps two working sets (queues, film chunk,
+ * sub-wavefront streams), each bound to the caller stream it was first used
+ * with: renders queued alternately on two streams overlap (one drains while
+ * the next starts); a third stream takes over the least recently used set. */
 spt_status spt_render_async(spt_scene scene, const spt_render_params* params, float* film_dev, void* stream,
                             uint64_t* ticket);
 spt_status spt_render_wait(spt_scene scene, uint64_t ticket, spt_render_stats* stats);

@@ -135,12 +135,15 @@ struct Sub {
 
 // One render's working memory: path queues, counters and sub-wavefront
 // streams, the per-sample film chunk and the running sum.  A scene keeps two
-// (kWorkSets), used by alternate renders, so a render queued on another stream
-// can start while the previous one drains; a render waits for the last render
-// that used its set (free_ev), so any stream use stays race-free.
+// (kWorkSets), one per caller stream (pick_set), so a render queued on another
+// stream can start while the previous one drains; a render waits for the last
+// render that used its set (free_ev), so any stream use stays race-free.
 constexpr int kWorkSets = 2;
 struct WorkSet {
     Sub sub[kMaxStreams];
+    hipStream_t home = nullptr;         // the caller stream the set was first used with (bound)
+    bool bound = false;
+    uint64_t last_ticket = 0;           // the last render that used the set
     size_t film_cap = 0, acc_cap = 0;
     char* film = nullptr;               // per-sample contributions of a chunk (bytes or RGB floats)
     float* acc = nullptr;               // [3][P] running sum across chunks
@@ -165,6 +168,29 @@ struct WorkSet {
 
 struct Workspace {
     WorkSet sets[kWorkSets];
+    // The working set of a render on caller stream `s`: the set bound to that
+    // stream, else one never used, else the least recently used (rebound).
+    // HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues as they are
+    // first used, and a set's sub-wavefront streams were mapped beside the
+    // caller stream they first ran with (sub 0 is the caller's own): the same
+    // set on another caller stream can put two of the four sub-wavefronts on
+    // one queue, which serialises them (config 3 / 4: -17 % / -16 %,
+    // profiles/r03_queues/).
+    WorkSet& pick_set(hipStream_t s) {
+        WorkSet* lru = &sets[0];
+        for (WorkSet& w : sets)
+            if (w.bound && w.home == s) return w;
+        for (WorkSet& w : sets)
+            if (!w.bound) {
+                w.bound = true;
+                w.home = s;
+                return w;
+            }
+        for (WorkSet& w : sets)
+            if (w.last_ticket < lru->last_ticket) lru = &w;
+        lru->home = s;
+        return *lru;
+    }
     size_t jump_cap = 0;
     PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps (read-only)
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
@@ -1687,7 +1713,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
     rs.paths_in_flight = (uint32_t)C;
-    WorkSet& ws = sc->ws.sets[sc->ws.next_ticket % kWorkSets];
+    WorkSet& ws = sc->ws.pick_set(stream);
+    ws.last_ticket = sc->ws.next_ticket;
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P);
     if (st) return st;
     if ((st = ensure_jumps(sc->ws, p.spp, p.max_depth))) return st;

@@ -36,6 +36,8 @@ for s in "$@"; do
     bench1gq) run bench1gq 600 env SPT_BUILD=gpu python bench.py --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench10) run bench10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench1f) run bench1f 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --pipeline fused ;;
     bench0|bench2|bench3|bench4) run $s 600 python bench.py --config ${s#bench} --steps 2 --warmup 1 ;;
     bench2q|bench3q|bench4q) c=${s#bench}; run $s 600 python bench.py --config ${c%q} --steps 2 --warmup 1 --no-cpu-baseline ;;
     benchwf) for wf in ${WFS:-1048576 4194304 8388608}; do run benchwf$wf 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --wavefront $wf; done ;;
