@@ -321,10 +321,10 @@ def test_render_async_limit(gscene):
 
 
 def test_render_async_two_streams(gscene, oscene):
-    """Renders queued on alternating streams use alternating working sets and
-    may overlap on the GPU; each waits for the last render of its set, so
-    back-to-back renders of different sizes and pipelines on two streams give
-    the oracle's images bit for bit."""
+    """Renders queued on two streams take the working set bound to their
+    stream and may overlap on the GPU; each waits for the last render of its
+    set, so back-to-back renders of different sizes and pipelines on two
+    streams give the oracle's images bit for bit."""
     jobs = [(48, 40, 7, 4, "wavefront"), (32, 24, 4, 3, "fused"), (40, 40, 5, 2, "fused"), (24, 20, 2, 8, "wavefront"),
             (33, 17, 3, 1, "fused")]
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -334,6 +334,25 @@ def test_render_async_two_streams(gscene, oscene):
                                            stream=streams[(i // 2) % 2])  # sets and streams out of phase
         queued.append((film, ticket))
     torch.cuda.synchronize()
+    for (w, h, spp, depth, pipe), (film, ticket) in zip(jobs, queued):
+        st = gscene.render_wait(ticket)
+        assert_work_complete(st, h, w, spp)
+        ref, _ = oracle_render(oscene, w, h, spp, depth)
+        np.testing.assert_array_equal(film.cpu().numpy(), ref)
+
+
+def test_render_async_three_streams(gscene, oscene):
+    """A third caller stream takes over the least recently used working set
+    (Workspace::pick_set): renders cycling over three streams, and the null
+    stream between them, still give the oracle's images and complete work."""
+    jobs = [(40, 32, 3, 4, "wavefront"), (24, 24, 2, 3, "wavefront"), (32, 16, 4, 2, "fused"), (40, 32, 3, 4, "wavefront"),
+            (16, 40, 2, 5, "wavefront"), (24, 24, 2, 3, "fused"), (32, 16, 4, 2, "wavefront")]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+    queued = []
+    for i, (w, h, spp, depth, pipe) in enumerate(jobs):
+        s = None if i == 4 else streams[i % 3]
+        film, ticket = gscene.render_async(sptamd.make_params(w, h, spp, depth, pipeline=pipe), stream=s)
+        queued.append((film, ticket))
     for (w, h, spp, depth, pipe), (film, ticket) in zip(jobs, queued):
         st = gscene.render_wait(ticket)
         assert_work_complete(st, h, w, spp)
