@@ -911,6 +911,17 @@ __device__ __forceinline__ Pcg32 path_rng(uint64_t initstate, uint32_t gpix, con
 // refill hands consecutive lanes consecutive pixels of one sample (coherent
 // camera rays).  RNG: the pixel's PCG32 stream (main.cpp:376) advanced to the
 // sample's first draw, s * (4 + 2D) draws (main.cpp:395,396,413 per sample).
+// Refill grid: at most kRefillMaxBlocks blocks striding over the new paths
+// instead of one thread per queue slot the host may have to fill (the host
+// sizes it before it knows how many paths ended): config 1 +0.9 %, config 2
+// +1.8 % (profiles/r03_tune/knob_sweep.log).
+#ifndef SPT_REFILL_STRIDE
+#define SPT_REFILL_STRIDE 1
+#endif
+#ifndef SPT_REFILL_MAX_BLOCKS
+#define SPT_REFILL_MAX_BLOCKS 4096
+#endif
+constexpr uint32_t kRefillMaxBlocks = SPT_REFILL_MAX_BLOCKS;
 template <int kMode>
 __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     const uint32_t surv = *a.surv;
@@ -932,19 +943,27 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         }
         if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
     }
+#if SPT_REFILL_STRIDE
+    for (uint32_t j = i; j < total; j += gridDim.x * 256u) {
+#else
     if (i >= total) return;
-    uint32_t s, q, lx, ly;
-    work_item((uint32_t)(cur + i - (uint64_t)a.chunk_s0 * a.P), a.chunk_s0, a.chunk_ns, a.P, a.work_order != 0, s, q);
-    work_pixel(q, a.W, a.P, a.pixel_block, lx, ly);
-    const uint32_t p = ly * a.W + lx;
-    const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
-    const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
-    Pcg32 rng;
-    rng.seed(a.initstate, (uint64_t)gpix);                   // main.cpp:376
-    rng.state = pcg_apply(a.sample_jump[s], rng.state, rng.inc);
-    V3 o, d;
-    camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
-    store_path<kMode>(a.q, surv + i, o, d, p, s << kMetaDepthBits, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f, 0.0f);  // main.cpp:391
+    {
+        const uint32_t j = i;
+#endif
+        uint32_t s, q, lx, ly;
+        work_item((uint32_t)(cur + j - (uint64_t)a.chunk_s0 * a.P), a.chunk_s0, a.chunk_ns, a.P, a.work_order != 0, s,
+                  q);
+        work_pixel(q, a.W, a.P, a.pixel_block, lx, ly);
+        const uint32_t p = ly * a.W + lx;
+        const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
+        const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
+        Pcg32 rng;
+        rng.seed(a.initstate, (uint64_t)gpix);                   // main.cpp:376
+        rng.state = pcg_apply(a.sample_jump[s], rng.state, rng.inc);
+        V3 o, d;
+        camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
+        store_path<kMode>(a.q, surv + j, o, d, p, s << kMetaDepthBits, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f, 0.0f);  // main.cpp:391
+    }
 }
 
 // ----------------------------------------------------------------- shade
@@ -1612,7 +1631,11 @@ hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* l
 }
 
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s) {
+#if SPT_REFILL_STRIDE
+    const dim3 g(std::min<uint32_t>(blocks_for(grid_items > 0 ? grid_items : 1, 256), kRefillMaxBlocks)), b(256);
+#else
     const dim3 g(blocks_for(grid_items > 0 ? grid_items : 1, 256)), b(256);
+#endif
     if (a.mode == kModeEmit) hipLaunchKernelGGL(refill_kernel<kModeEmit>, g, b, 0, s, a);
     else if (a.mode == kModeAlbedo) hipLaunchKernelGGL(refill_kernel<kModeAlbedo>, g, b, 0, s, a);
     else hipLaunchKernelGGL(refill_kernel<kModeUnit>, g, b, 0, s, a);
