@@ -25,11 +25,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 
-# Eight hardware queues per process (HIP's default is 4): the two working sets'
-# sub-wavefront streams (four each, spt.h spt_render_async) then run on queues of
-# their own while consecutive renders overlap (config 1 +1.9 %).
-# The HIP runtime reads it when it starts, so it is set before torch is imported.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Eight hardware queues per process (HIP's default, and the GPU box's setting, is
+# 4): the two working sets' sub-wavefront streams (four each, spt.h
+# spt_render_async) then run on queues of their own while consecutive renders
+# overlap (config 1 +1.9 %).  The HIP runtime reads it when it
+# starts, so it is set before torch is imported; SPT_HW_QUEUES overrides it.
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SPT_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_JSON = os.path.join(ROOT, "profiles", "isect_pmc.json")  # tools/pmc_isect.sh output

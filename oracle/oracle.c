@@ -905,6 +905,117 @@ static inline void draw2(pcg32_t* rng, int order, float* x, float* y) {
     if (order == 0) { *y = a; *x = b; } else { *x = a; *y = b; }
 }
 
+/* One sample of one pixel (main.cpp:391-426): its radiance in L; rng is the
+ * pixel's stream at this sample's first draw.  rec (may be NULL) records each
+ * cast's ray and hit, for tests/diag that follow one path (oracle_trace_sample). */
+typedef struct {
+    float* rays;     /* [max_depth][6]: origin, direction */
+    int32_t* ids;    /* [max_depth] hit id (-1 miss) */
+    float* tuv;      /* [max_depth][3] */
+    int32_t n;
+} cast_rec;
+
+static void sample_path(const oscene* s, const oracle_params* p, const camera_t* cam, pcg32_t* rng, uint32_t pixel,
+                        int32_t px, int32_t py, int32_t smp, float L[3], long long* casts, cast_rec* rec) {
+    float contrib[3] = {1.0f, 1.0f, 1.0f};                        /* main.cpp:391 */
+    L[0] = L[1] = L[2] = 0.0f;  /* this sample's radiance, added to film once */
+    int active = 1;                                               /* main.cpp:392 */
+    float xi_x, xi_y;
+    draw2(rng, p->rng_order, &xi_x, &xi_y);                       /* main.cpp:395 */
+    v3 o = camera_sample_pos(cam, xi_x, xi_y);
+    draw2(rng, p->rng_order, &xi_x, &xi_y);                       /* main.cpp:396 */
+    v3 d = camera_sample_dir(cam, px, py, o, xi_x, xi_y);
+    for (int32_t j = 0; j < p->max_depth; j++) {                  /* main.cpp:399 */
+        ohit h; h.id = -1;
+        if (active) {                                              /* main.cpp:402-404 */
+            wray r;
+            r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z;
+            r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z;
+            wray_setup(&r);
+            trace(s, &r, 0.001f, 1e20f, 1, &h);                   /* ray.h:15-17 */
+            if (s->nsph) trace_spheres(s, o, d, 0.001f, 0, &h);   /* smallpt's spheres */
+            (*casts)++;
+            if (rec) {
+                float* q = rec->rays + rec->n * 6;
+                q[0] = o.x; q[1] = o.y; q[2] = o.z; q[3] = d.x; q[4] = d.y; q[5] = d.z;
+                rec->ids[rec->n] = h.id;
+                rec->tuv[rec->n * 3] = h.id == -1 ? 0.0f : h.t;
+                rec->tuv[rec->n * 3 + 1] = h.id == -1 ? 0.0f : h.u;
+                rec->tuv[rec->n * 3 + 2] = h.id == -1 ? 0.0f : h.v;
+                rec->n++;
+            }
+            if (h.id == -1) {                                     /* main.cpp:407 */
+                for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * p->env[k];
+            } else if (s->emission) {
+                /* emitted radiance at every hit (smallpt's obj.e; the
+                 * reference has no emitters — SURVEY §8f row 3) */
+                int32_t me = h.id >= 0 ? s->mat[h.id] : s->sph_mat[-2 - h.id];
+                if (me >= 0 && me < s->nemit)
+                    for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * s->emission[me * 3 + k];
+            }
+        }
+        active = active && (h.id != -1);                          /* main.cpp:410 */
+        draw2(rng, p->rng_order, &xi_x, &xi_y);                   /* main.cpp:413 (always drawn) */
+        if (!active) continue;
+        /* optix_backend.h:469 (position), :483-484 (interpolated shading normal) */
+        const int sph = h.id < -1;
+        float w = (1.0f - h.u) - h.v;
+        v3 n = mk(0.0f, 0.0f, 0.0f);
+        if (!sph) {
+            const float* nv = &s->n[(int64_t)h.id * 9];
+            n = mk((w * nv[0] + h.u * nv[3]) + h.v * nv[6],
+                   (w * nv[1] + h.u * nv[4]) + h.v * nv[7],
+                   (w * nv[2] + h.u * nv[5]) + h.v * nv[8]);
+        }
+        v3 hp = mk(o.x + h.t * d.x, o.y + h.t * d.y, o.z + h.t * d.z);
+        int32_t m = sph ? s->sph_mat[-2 - h.id] : s->mat[h.id];
+        float sw = 1.0f;   /* the scatter weight (glass), applied after roulette */
+        v3 out;
+        if (!s->nsph && !s->nkind) {
+            frame3 f = frame_from_normal(n);                      /* main.cpp:414 */
+            v3 lo = cosine_hemisphere(xi_x, xi_y);                /* main.cpp:418, :109-117 */
+            out = to_world(&f, lo);                               /* main.cpp:419 */
+        } else {
+            out = scatter(s, material_kind(s, m), h.id, d, hp, n, xi_x, xi_y, &sw);
+        }
+        int32_t mt = m;
+        if (m < 0 || m >= s->nmat) m = 0;
+        float refl[3] = {s->albedo[m * 3], s->albedo[m * 3 + 1], s->albedo[m * 3 + 2]};
+#ifdef ORACLE_ALT_TEX1X1
+        int tex = 1;  /* every material is an ImageTexture: a 1x1 image of its colour (main.cpp:40-44) */
+        const float* timg = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_rgb[mt] : &s->albedo[m * 3];
+        int32_t tw = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_w[mt] : 1;
+        int32_t th = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_h[mt] : 1;
+#else
+        int tex = mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0;
+        const float* timg = tex ? s->tex_rgb[mt] : NULL;
+        int32_t tw = tex ? s->tex_w[mt] : 0, th = tex ? s->tex_h[mt] : 0;
+#endif
+        if (tex) {
+            /* LambertBsdf::sample -> m_reflectance->eval(texcoord) (main.cpp:109-117):
+             * texcoord = barycentric_interpolate (optix_backend.h:395-401, add_math.h:4-7) */
+            float tu = 0.0f, tv = 0.0f;
+            if (s->tc && !sph) {
+                const float* c = &s->tc[(int64_t)h.id * 6];
+                tu = (w * c[0] + h.u * c[2]) + h.v * c[4];
+                tv = (w * c[1] + h.u * c[3]) + h.v * c[5];
+            }
+            texture_eval(timg, tw, th, tu, tv, refl);
+        }
+        for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * refl[k];   /* :422 */
+        o = hp;                                                   /* main.cpp:423 */
+        d = out;                                                  /* main.cpp:424 */
+        if (j + 1 >= p->rr_start_depth && j + 1 < p->max_depth) {
+            float q = fmaxf(contrib[0], fmaxf(contrib[1], contrib[2]));
+            if (q < 1.0f) {
+                if (rr_uniform(pixel, (uint32_t)smp, (uint32_t)j) >= q) { active = 0; continue; }
+                for (int k = 0; k < 3; k++) contrib[k] = contrib[k] / q;
+            }
+        }
+        for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * sw;  /* smallpt's glass weight */
+    }
+}
+
 static void render_pixel(void* c_, int64_t li) {
     render_ctx* c = (render_ctx*)c_;
     const oracle_params* p = c->p;
@@ -919,94 +1030,8 @@ static void render_pixel(void* c_, int64_t li) {
     float film[3] = {0.0f, 0.0f, 0.0f};
     long long casts = 0;
     for (int32_t smp = 0; smp < p->spp; smp++) {                  /* main.cpp:385 */
-        float contrib[3] = {1.0f, 1.0f, 1.0f};                    /* main.cpp:391 */
-        float L[3] = {0.0f, 0.0f, 0.0f};  /* this sample's radiance, added to film once */
-        int active = 1;                                           /* main.cpp:392 */
-        float xi_x, xi_y;
-        draw2(&rng, p->rng_order, &xi_x, &xi_y);                  /* main.cpp:395 */
-        v3 o = camera_sample_pos(&c->cam, xi_x, xi_y);
-        draw2(&rng, p->rng_order, &xi_x, &xi_y);                  /* main.cpp:396 */
-        v3 d = camera_sample_dir(&c->cam, px, py, o, xi_x, xi_y);
-        for (int32_t j = 0; j < p->max_depth; j++) {              /* main.cpp:399 */
-            ohit h; h.id = -1;
-            if (active) {                                          /* main.cpp:402-404 */
-                wray r;
-                r.o[0] = o.x; r.o[1] = o.y; r.o[2] = o.z;
-                r.d[0] = d.x; r.d[1] = d.y; r.d[2] = d.z;
-                wray_setup(&r);
-                trace(s, &r, 0.001f, 1e20f, 1, &h);               /* ray.h:15-17 */
-                if (s->nsph) trace_spheres(s, o, d, 0.001f, 0, &h);   /* smallpt's spheres */
-                casts++;
-                if (h.id == -1) {                                 /* main.cpp:407 */
-                    for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * p->env[k];
-                } else if (s->emission) {
-                    /* emitted radiance at every hit (smallpt's obj.e; the
-                     * reference has no emitters — SURVEY §8f row 3) */
-                    int32_t me = h.id >= 0 ? s->mat[h.id] : s->sph_mat[-2 - h.id];
-                    if (me >= 0 && me < s->nemit)
-                        for (int k = 0; k < 3; k++) L[k] = L[k] + contrib[k] * s->emission[me * 3 + k];
-                }
-            }
-            active = active && (h.id != -1);                      /* main.cpp:410 */
-            draw2(&rng, p->rng_order, &xi_x, &xi_y);              /* main.cpp:413 (always drawn) */
-            if (!active) continue;
-            /* optix_backend.h:469 (position), :483-484 (interpolated shading normal) */
-            const int sph = h.id < -1;
-            float w = (1.0f - h.u) - h.v;
-            v3 n = mk(0.0f, 0.0f, 0.0f);
-            if (!sph) {
-                const float* nv = &s->n[(int64_t)h.id * 9];
-                n = mk((w * nv[0] + h.u * nv[3]) + h.v * nv[6],
-                       (w * nv[1] + h.u * nv[4]) + h.v * nv[7],
-                       (w * nv[2] + h.u * nv[5]) + h.v * nv[8]);
-            }
-            v3 hp = mk(o.x + h.t * d.x, o.y + h.t * d.y, o.z + h.t * d.z);
-            int32_t m = sph ? s->sph_mat[-2 - h.id] : s->mat[h.id];
-            float sw = 1.0f;   /* the scatter weight (glass), applied after roulette */
-            v3 out;
-            if (!s->nsph && !s->nkind) {
-                frame3 f = frame_from_normal(n);                  /* main.cpp:414 */
-                v3 lo = cosine_hemisphere(xi_x, xi_y);            /* main.cpp:418, :109-117 */
-                out = to_world(&f, lo);                           /* main.cpp:419 */
-            } else {
-                out = scatter(s, material_kind(s, m), h.id, d, hp, n, xi_x, xi_y, &sw);
-            }
-            int32_t mt = m;
-            if (m < 0 || m >= s->nmat) m = 0;
-            float refl[3] = {s->albedo[m * 3], s->albedo[m * 3 + 1], s->albedo[m * 3 + 2]};
-#ifdef ORACLE_ALT_TEX1X1
-            int tex = 1;  /* every material is an ImageTexture: a 1x1 image of its colour (main.cpp:40-44) */
-            const float* timg = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_rgb[mt] : &s->albedo[m * 3];
-            int32_t tw = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_w[mt] : 1;
-            int32_t th = (mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0) ? s->tex_h[mt] : 1;
-#else
-            int tex = mt >= 0 && mt < s->ntex && s->tex_w[mt] > 0;
-            const float* timg = tex ? s->tex_rgb[mt] : NULL;
-            int32_t tw = tex ? s->tex_w[mt] : 0, th = tex ? s->tex_h[mt] : 0;
-#endif
-            if (tex) {
-                /* LambertBsdf::sample -> m_reflectance->eval(texcoord) (main.cpp:109-117):
-                 * texcoord = barycentric_interpolate (optix_backend.h:395-401, add_math.h:4-7) */
-                float tu = 0.0f, tv = 0.0f;
-                if (s->tc && !sph) {
-                    const float* c = &s->tc[(int64_t)h.id * 6];
-                    tu = (w * c[0] + h.u * c[2]) + h.v * c[4];
-                    tv = (w * c[1] + h.u * c[3]) + h.v * c[5];
-                }
-                texture_eval(timg, tw, th, tu, tv, refl);
-            }
-            for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * refl[k];   /* :422 */
-            o = hp;                                               /* main.cpp:423 */
-            d = out;                                              /* main.cpp:424 */
-            if (j + 1 >= p->rr_start_depth && j + 1 < p->max_depth) {
-                float q = fmaxf(contrib[0], fmaxf(contrib[1], contrib[2]));
-                if (q < 1.0f) {
-                    if (rr_uniform(pixel, (uint32_t)smp, (uint32_t)j) >= q) { active = 0; continue; }
-                    for (int k = 0; k < 3; k++) contrib[k] = contrib[k] / q;
-                }
-            }
-            for (int k = 0; k < 3; k++) contrib[k] = contrib[k] * sw;  /* smallpt's glass weight */
-        }
+        float L[3];
+        sample_path(s, p, &c->cam, &rng, pixel, px, py, smp, L, &casts, NULL);
         /* Without emitters L is 0 or contrib * env: the same film sum as the
          * reference's per-miss film += contrib (main.cpp:407). */
         for (int k = 0; k < 3; k++) film[k] = film[k] + L[k];
@@ -1014,6 +1039,25 @@ static void render_pixel(void* c_, int64_t li) {
     int64_t npx = c->nrow_pixels;
     for (int k = 0; k < 3; k++) c->film[k * npx + li] = film[k] / (float)p->spp; /* main.cpp:429 */
     atomic_fetch_add(&c->casts, casts);
+}
+
+/* Diagnostics (tools/diag_parity.py): the casts of sample `smp` of pixel (px,
+ * py) — each cast's ray and closest hit — and the sample's radiance.  Returns
+ * the number of casts (at most max_depth). */
+int32_t oracle_trace_sample(void* scene, const oracle_params* p, int32_t px, int32_t py, int32_t smp, float* rays,
+                            int32_t* ids, float* tuv, float* L3) {
+    const oscene* s = (const oscene*)scene;
+    camera_t cam;
+    camera_setup(&cam, p);
+    uint32_t pixel = (uint32_t)py * (uint32_t)p->width + (uint32_t)px;
+    pcg32_t rng;
+    pcg32_seed(&rng, p->rng_initstate, (uint64_t)pixel);
+    long long casts = 0;
+    float L[3];
+    for (int32_t k = 0; k < smp; k++) sample_path(s, p, &cam, &rng, pixel, px, py, k, L, &casts, NULL);
+    cast_rec rec = {rays, ids, tuv, 0};
+    sample_path(s, p, &cam, &rng, pixel, px, py, smp, L3, &casts, &rec);
+    return rec.n;
 }
 
 int oracle_render(void* scene, const oracle_params* p, const int32_t* rows, int32_t nrows,

@@ -65,6 +65,9 @@ int oracle_render(void* scene, const oracle_params* p, const int32_t* rows, int3
 /* Known-answer helpers. */
 void oracle_pcg32_seq(uint64_t initstate, uint64_t initseq, uint32_t* out, int32_t n);
 void oracle_pcg32_floats(uint64_t initstate, uint64_t initseq, float* out, int32_t n);
+/* tools/diag_parity.py: the casts (ray, closest hit) of one sample of one pixel */
+int32_t oracle_trace_sample(void* scene, const oracle_params* p, int32_t px, int32_t py, int32_t smp, float* rays,
+                            int32_t* ids, float* tuv, float* L3);
 void oracle_camera_ray(const oracle_params* p, int32_t px, int32_t py, const float* xi4,
                        float* org3, float* dir3, float* basis9);
 void oracle_sincos(float x, float* s, float* c);
