@@ -719,8 +719,17 @@ static void trace(const oscene* s, const wray* r, float tmin, float tmax, int cl
     while (sp) {
         const onode* nd = &s->nodes[stack[--sp]];
         /* the current hit padded like the exit planes: boxes entered at the
-         * hit's t (ties at shared edges / vertices) are still visited */
+         * hit's t (ties at shared edges / vertices) are still visited.  Boxes
+         * the ray leaves before tmin are culled, as on the GPU: a Woop hit a
+         * little past tmin outside its triangle's own box (origin on the
+         * triangle's plane) is then kept or not by the tree's box sizes
+         * (ORACLE_BOX_CULL_NEG_TMIN culls at -|tmin| and keeps it,
+         * like the brute-force scan) */
+#ifdef ORACLE_BOX_CULL_NEG_TMIN
+        if (!box_test(r, nd, fminf(tmin, -tmin), h->t * BOX_PAD)) continue;
+#else
         if (!box_test(r, nd, tmin, h->t * BOX_PAD)) continue;
+#endif
         if (nd->count) {
             for (int32_t i = 0; i < nd->count; i++) {
                 consider(s, r, s->prims[nd->left + i], tmin, h);

@@ -59,6 +59,8 @@ def _load(path=LIB_PATH):
     lib.oracle_cosine_hemisphere.argtypes = [c_float, c_float, vp]
     lib.oracle_disk_from_square.argtypes = [c_float, c_float, vp]
     lib.oracle_frame_to_world.argtypes = [vp, vp, vp]
+    lib.oracle_trace_sample.restype = c_int32
+    lib.oracle_trace_sample.argtypes = [vp, POINTER(OracleParams), c_int32, c_int32, c_int32, vp, vp, vp, vp]
     return lib
 
 

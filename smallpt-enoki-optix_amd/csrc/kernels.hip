@@ -181,11 +181,24 @@ __device__ __forceinline__ void slab(float p0, float p1, float o, float inv, flo
     t1 = (p1 - o) * inv;
 }
 
+// Box culling lower bound (tbox).  Default: boxes the ray leaves before tmin
+// are culled.  A ray leaving a surface (origin on a triangle's plane) can get
+// a Woop hit a little past tmin that lies outside the triangle's own box (the
+// t of a near-coplanar origin is all rounding); whether a tree keeps it then
+// depends on how tight its boxes are.  SPT_BOX_CULL_TMIN=0
+// culls at -|tmin| instead and keeps such hits like a brute-force scan, at
+// -12 % on config 1 and -3.5 % on config 4 (profiles/r03_parity/), so it is
+// an experiment, not the default.
+#ifndef SPT_BOX_CULL_TMIN
+#define SPT_BOX_CULL_TMIN 1
+#endif
+__device__ __forceinline__ float box_tmin(float tmin) { return SPT_BOX_CULL_TMIN ? tmin : fminf(tmin, -tmin); }
+
 struct Tracer {
     static constexpr int kMinWaves = 1;
     WoopRay wr;
     V3 o;
-    float ix, iy, iz, tmin;
+    float ix, iy, iz, tmin, tbox;
     int32_t node;
     uint32_t sp;
     bool anyhit;
@@ -199,6 +212,7 @@ struct Tracer {
         wr = woop_setup(o_, d);
         ix = 1.0f / d.x; iy = 1.0f / d.y; iz = 1.0f / d.z;
         tmin = tmin_;
+        tbox = box_tmin(tmin_);
         anyhit = anyhit_;
         node = sc.empty ? kDone : 0;
         sp = 0;
@@ -227,13 +241,13 @@ struct Tracer {
             slab(n0.x, n0.y, o.x, ix, a0, a1);
             slab(n0.z, n0.w, o.y, iy, b0, b1);
             slab(n2.x, n2.y, o.z, iz, c0, c1);
-            const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), tmin));
+            const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), tbox));
             const float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1)) * kBoxPad;
             float d0, d1, e0, e1, f0, f1;
             slab(n1.x, n1.y, o.x, ix, d0, d1);
             slab(n1.z, n1.w, o.y, iy, e0, e1);
             slab(n2.z, n2.w, o.z, iz, f0, f1);
-            const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fmaxf(fminf(f0, f1), tmin));
+            const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fmaxf(fminf(f0, f1), tbox));
             const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1)) * kBoxPad;
             // the current hit padded like the exit planes: a box entered at the
             // hit's t (a tie at a shared edge or vertex) is still visited, so
@@ -322,7 +336,7 @@ struct Tracer8T {
     static constexpr int kMinWaves = kW == 6 ? SPT_ISECT_WAVES6 : SPT_ISECT_WAVES;
     WoopRay wr;
     V3 o;
-    float ix, iy, iz, tmin;
+    float ix, iy, iz, tmin, tbox;
     uint32_t oct_rep;  // the ray's inverted octant (0..7) replicated in every byte
     // node group: unvisited hit children in bits 24..31 (bit 24 + (slot ^
     // octant)), the child-group word in bits 0..23 (child s of a node sits at
@@ -391,6 +405,7 @@ struct Tracer8T {
         const uint32_t oct_inv = oct ^ 7u;
         oct_rep = oct_inv * 0x01010101u;
         tmin = tmin_;
+        tbox = box_tmin(tmin_);
         anyhit = anyhit_;
         nhits = 1u << (24u + oct_inv);  // the root: slot 0 of a virtual group at node 0
         tbase = 0;
@@ -463,7 +478,7 @@ struct Tracer8T {
             const float txy = fmaf((float)(((lo ? xyl : e45y) >> (lo ? sh : sh + 16u)) & 0xffu), ay, byx);
             const float tez = fmaf((float)(((lo ? ezl : e45z) >> sh) & 0xffu), az, bze);
             const float txz = fmaf((float)(((lo ? xzl : e45z) >> (lo ? sh : sh + 16u)) & 0xffu), az, bzx);
-            const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tmin));
+            const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tbox));
             const float tf = fminf(fminf(txx, txy), fminf(txz, h.t));
             const uint32_t mw = lo ? mlo : mhi;
             const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);
@@ -502,7 +517,7 @@ struct Tracer8T {
             const float txy = fmaf((float)(((lo ? xyl : xyh) >> sh) & 0xffu), ay, byx);
             const float tez = fmaf((float)(((lo ? ezl : ezh) >> sh) & 0xffu), az, bze);
             const float txz = fmaf((float)(((lo ? xzl : xzh) >> sh) & 0xffu), az, bzx);
-            const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tmin));
+            const float tn = fmaxf(fmaxf(tex, tey), fmaxf(tez, tbox));
             const float tf = fminf(fminf(txx, txy), fminf(txz, h.t));
             const uint32_t mw = lo ? mlo : mhi;
             const uint32_t bits = __builtin_amdgcn_ubfe(mw, sh + 5u, 3u) << __builtin_amdgcn_ubfe(mw, sh, 5u);

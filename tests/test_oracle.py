@@ -393,3 +393,23 @@ def test_glass_sphere_conserves_energy():
     f, _ = sc.render(O.reference_params(16, 16, 64, 24, rr_start_depth=99, env=(1, 1, 1)))
     assert abs(f.mean() - 1.0) < 0.03, f.mean()
     assert f.std() > 0.05      # the weights differ per sample
+
+
+
+def test_hit_past_tmin_outside_triangle_box_known_case():
+    """Pinned known case (config 4's city_synth, found by tools/diag_parity.py):
+    a ray leaving a column surface, its origin on the triangle's plane, gets a
+    Woop hit at t = 0.0015 (past tmin = 0.001) outside the triangle's own box,
+    which the ray leaves at t = 0.0003.  Brute force keeps the hit; a tree
+    that culls boxes left before tmin (the oracle's tight BVH2, the GPU's
+    default) drops it, while a looser box (the GPU's quantised BVH8 in the
+    full scene) keeps it: one sample of 10.5M paths differed."""
+    pos = np.array([[-0.249440879, -1, 8.8333292], [-0.212132037, 5, 8.78786755], [-0.249440879, 5, 8.8333292]],
+                   np.float32)
+    m = {"pos_tri": np.array([[0, 1, 2]], np.int32), "pos": pos}
+    o = np.array([[-0.24933969974517822], [1.7225027084350586], [8.833206176757812]], np.float32)
+    d = np.array([[-0.3425644636154175], [0.8412052392959595], [0.4182586371898651]], np.float32)
+    brute = O.OracleScene(m, use_bvh=False).intersect(o, d)
+    bvh = O.OracleScene(m).intersect(o, d)
+    assert brute[0][0] == 0 and abs(float(brute[1][0]) - 0.0015052289) < 1e-9
+    assert bvh[0][0] == -1

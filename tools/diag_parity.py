@@ -12,7 +12,7 @@ brute-force oracle scene for the closest hit of each of those rays.
 from __future__ import annotations
 
 import argparse
-import ctypes
+import ctypes  # noqa: F401 (ctypes.byref)
 import json
 import os
 import sys
@@ -76,7 +76,6 @@ def main():
                       "pixels": pix[:32]}), flush=True)
     brute = O.OracleScene(mesh, use_bvh=False, albedo=alb, emission=emi) if a.brute else None
     lib = osc.lib
-    lib.oracle_trace_sample.restype = ctypes.c_int32
     for (y, x) in pix[:a.max_pixels]:
         # the first sample count whose film value differs (one changed sample
         # changes every later prefix)
@@ -98,8 +97,8 @@ def main():
         ids = np.zeros(D, np.int32)
         tuv = np.zeros((D, 3), np.float32)
         L = np.zeros(3, np.float32)
-        n = lib.oracle_trace_sample(osc.h, ctypes.byref(p), ctypes.c_int32(x), ctypes.c_int32(y), ctypes.c_int32(s),
-                                    rays.ctypes.data, ids.ctypes.data, tuv.ctypes.data, L.ctypes.data)
+        n = lib.oracle_trace_sample(osc.h, ctypes.byref(p), x, y, s, rays.ctypes.data, ids.ctypes.data,
+                                    tuv.ctypes.data, L.ctypes.data)
         o = np.ascontiguousarray(rays[:n, :3].T)
         d = np.ascontiguousarray(rays[:n, 3:].T)
         rr = sptamd.Ray3.make(o, d)
