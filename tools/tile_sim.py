@@ -55,7 +55,8 @@ def main():
         rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
         films = [torch.empty((3, rows, W), dtype=torch.float32, device="cuda") for _ in range(2)]
         streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
-        scene.render(p, film=films[0])
+        for k in range(2):  # one setup render per stream (working set) before the timed steps, as bench.py
+            scene.render_wait(scene.render_async(p, film=films[k], stream=streams[k])[1])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if args.sync:
