@@ -11,8 +11,8 @@ BASELINE.json configs[i] (0 = the 256^2 x 4 spp plumbing run).
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Prints one JSON line (rank 0) with the metric, the isect kernel's roofline
-(HIP events on the render stream) and the CPU-oracle baseline timed on this
-host (N = 1 only).
+(HIP events on the render stream), the CPU-oracle baseline timed on this
+host, and the parity of the (assembled) image against that oracle render.
 """
 from __future__ import annotations
 
@@ -30,6 +30,8 @@ sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 # spt_render_async) then run on queues of their own while consecutive renders
 # overlap (config 1 +1.9 %).  The HIP runtime reads it when it
 # starts, so it is set before torch is imported; SPT_HW_QUEUES overrides it.
+# The line records the value requested and the one the environment had.
+HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SPT_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -37,7 +39,9 @@ PMC_JSON = os.path.join(ROOT, "profiles", "isect_pmc.json")  # tools/pmc_isect.s
 VALU_PEAK_G = 256 * 4 * 2.4 / 2  # wave64 VALU instr/s (G): 1024 SIMDs, 2 cycles each at 2.4 GHz (MI355X_MICROARCH.md)
 ISECT_BYTES_PER_CAST = 52      # queue idx 4 + ray 32 (o, d, tmin, tmax) in, hit 16 out
 KERNEL_BYTES_PER_CAST = 44     # what isect_queue_kernel moves: ray 24 + meta 4 in, hit 16 out
-FUSED_BYTES_PER_PATH = 12      # per-sample film RGB write
+# what render_fused_kernel itself moves per path: its per-sample
+# film write, one escape byte (the reference's unit mode) or an RGB float triple
+FUSED_BYTES_PER_PATH = {True: 1, False: 12}
 
 
 # BASELINE.json configs (index = position in "configs"); 1 is the headline.
@@ -262,8 +266,6 @@ def main():
     film = tg.tile_view()
     stream = torch.cuda.current_stream()
 
-    gather_ev = []
-
     def check_work(st):
         """Device-counted work of one render against the job (main.cpp:385-429
         renders every pixel x sample): paths started == paths ended == tile
@@ -281,9 +283,6 @@ def main():
     # (experiment knobs, tools/ov.sh): setup renders, one render at a time
     SETUP_RENDERS = int(os.environ.get("SPT_BENCH_SETUP", "2"))
     SYNC_STEPS = os.environ.get("SPT_BENCH_SYNC", "0") == "1"
-    # gather timing events, created once (recorded on the step's stream)
-    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(max(args.steps, 1))]
     # Consecutive steps alternate between two streams and two film buffers
     # (the library alternates two working sets), so a step's render can start
     # while the previous one drains; the gathers stay in step order.
@@ -291,36 +290,38 @@ def main():
     films = [film, tg.tile_view(1)]
     last_gather = [None]
 
-    def step(p, i=None, k=0):
+    def step(p, ev=None, k=0):
         """One step: the render of this rank's tile, queued (spt_render_async:
         the GPU runs from one step's render into the next without waiting for
         the host), then the tile gather behind it on the same stream, after the
-        previous step's gather.  Returns the render's ticket; its device
-        counters are collected after the loop."""
+        previous step's gather (timed by the event pair ev, if given).  Returns
+        the render's ticket; its device counters are collected after the loop."""
         s = streams[k % 2]
         with torch.cuda.stream(s):
             _, ticket = scene.render_async(p, film=films[k % 2], stream=s)
             if last_gather[0] is not None:
                 s.wait_event(last_gather[0])
-            if i is not None:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
-                gev[i][0].record(s)
+            if ev is not None:  # the tile gather (RCCL over xGMI at N > 1) on the render stream's clock
+                ev[0].record(s)
             tg.gather(k % 2)
             done = torch.cuda.Event()
             done.record(s)
             last_gather[0] = done
-            if i is not None:
-                gev[i][1].record(s)
-                gather_ev.append(gev[i])
+            if ev is not None:
+                ev[1].record(s)
         return ticket
 
-    def timed_loop(p, evs):
+    def timed_loop(p):
         """W untimed steps, then exactly K timed steps between barriers +
         synchronize; returns (max-over-ranks seconds, summed stats, last stats,
-        device-counted paths of all ranks).  Every step's work accounting is
-        checked once the timed region has ended.  Before the warmup, one setup
-        render per working set and stream (SETUP_RENDERS): their buffers are
-        allocated on first use, which W = 1 warmup step would leave to the
-        first timed step."""
+        device-counted [casts, continuations, paths] of all ranks, this loop's
+        mean gather ms).  Every step's work accounting is checked once the
+        timed region has ended.  Before the warmup, one setup render per
+        working set and stream (SETUP_RENDERS): their buffers are allocated on
+        first use, which W = 1 warmup step would leave to the first timed step."""
+        # this loop's own gather timing events (recorded on the step's stream)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
         for k in range(SETUP_RENDERS):
             check_work(scene.render_wait(step(p, k=k)))
         for w in range(args.warmup):
@@ -329,11 +330,13 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        evs.clear()
+        # the isect (fused) kernel's busy time: the union of every timed
+        # launch interval of the K renders, which overlap on two streams
+        scene.isect_busy_begin()
         t0 = time.perf_counter()
         tickets, sts = [], []
         for i in range(args.steps):
-            tickets.append(step(p, i, k=i))
+            tickets.append(step(p, evs[i], k=i))
             if SYNC_STEPS:
                 sts.append(scene.render_wait(tickets.pop(0)))
             if len(tickets) > 32:  # the library holds at most 64 uncollected renders
@@ -351,10 +354,12 @@ def main():
             for k in agg:
                 agg[k] += st[k]
         # consecutive renders overlap on the GPU (two streams, two working
-        # sets): the kernel's busy time is the union over the renders, each
-        # render's own union less its overlap with the next (on one clock)
-        for a_, b_ in zip(sts, sts[1:]):
-            agg["isect_busy_ms"] -= max(0.0, min(a_["isect_end_ms"], b_["isect_end_ms"]) - b_["isect_begin_ms"])
+        # sets): the kernel's busy time is the union of all their launch
+        # intervals on the scene's clock (spt_scene_isect_busy_end)
+        agg["isect_busy_ms"], nl = scene.isect_busy_end()
+        if nl != agg["isect_launches"]:
+            raise RuntimeError(f"isect intervals {nl} != timed launches {agg['isect_launches']}")
+        gather_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / max(1, len(evs))
         tot = [agg["ray_casts"], agg["continuations"], agg["paths"]]
         if world > 1:
             rdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
@@ -364,9 +369,9 @@ def main():
             tt = torch.tensor(tot, dtype=torch.float64, device=rdev)
             dist.all_reduce(tt, op=dist.ReduceOp.SUM)
             tot = [float(x) for x in tt.tolist()]
-        return elapsed, agg, sts[-1], tot
+        return elapsed, agg, sts[-1], tot, gather_ms
 
-    elapsed, agg, st, (agg_casts_all, agg_cont_all, paths) = timed_loop(params, gather_ev)
+    elapsed, agg, st, (agg_casts_all, agg_cont_all, paths), gather_ms = timed_loop(params)
     if paths != W * H * args.spp * args.steps:
         raise RuntimeError(f"device-counted paths {paths} != {W * H * args.spp * args.steps} (W x H x spp x steps)")
     image_main = tg.image.clone() if rank == 0 else None
@@ -377,18 +382,15 @@ def main():
     if world > 1 and st.get("fused") and args.pipeline == "auto":
         pw = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
                                 wavefront_paths=args.wavefront, timing=True, pipeline="wavefront", **kw)
-        main_gather = list(gather_ev)
-        w_el, w_agg, w_st, w_tot = timed_loop(pw, gather_ev)
-        gather_ev[:] = main_gather
+        w_el, w_agg, w_st, w_tot, w_gather_ms = timed_loop(pw)
         w_paths = w_tot[2]
         wave_leg = {"pipeline": "wavefront", "value": round(w_paths / w_el / 1e6, 3),
                     "ms_per_step": round(w_el / args.steps * 1e3, 3), "streams": w_st.get("streams"),
                     "isect_busy_ms_per_step_rank0": round(w_agg["isect_busy_ms"] / args.steps, 4),
-                    "paths_device_counted": int(w_paths)}
+                    "paths_device_counted": int(w_paths), "gather_ms": round(w_gather_ms, 4)}
         if rank == 0 and image_main is not None:
             wave_leg["image_equal_to_fused"] = bool(torch.equal(image_main, tg.image))
     value = paths / elapsed / 1e6
-    gather_ms = sum(e0.elapsed_time(e1) for e0, e1 in gather_ev) / max(1, len(gather_ev))
     if rank == 0:
         # Roofline of the dominant kernel.  Wavefront:
         # isect_queue_kernel, SURVEY §8(d)'s 52 B per ray cast.  The K
@@ -398,9 +400,11 @@ def main():
         # kernel occupies the chip, <= ms_per_step.  `per_launch` keeps the
         # per-launch figure (a 1/K-chip rate when K > 1).  Fused:
         # render_fused_kernel runs the whole path (trace + shade + bounce) in
-        # registers, so its unit is the path and its bytes are SURVEY §8(d)'s
-        # whole-path model B_path = 84 + 120 S + 60 C (what the wavefront moves
-        # for the same path) over the fused launches' busy time.
+        # registers, so its unit is the path and its algorithmic bytes are
+        # what it moves, the per-sample film write (1 B in the reference's
+        # unit mode, 12 B of RGB otherwise); SURVEY §8(d)'s whole-path model
+        # B_path = 84 + 120 S + 60 C (what the wavefront moves for the same
+        # path) is reported beside it as `equivalent_wavefront`.
         fused = bool(st.get("fused"))
         work_order = {1: "sample-major", 2: "pixel-major"}.get(st.get("work_order"), "?")
         if scene.backend.config["work_order"] == 0:
@@ -411,15 +415,23 @@ def main():
         s_bar = agg_casts_all / paths
         c_bar = agg_cont_all / paths
         b_path = 84.0 + 120.0 * s_bar + 60.0 * c_bar
+        unit_mode = not args.smallpt  # albedo 1, no emitters: the reference's case (one escape byte per path)
         if fused:
-            bytes_per_unit = kernel_bytes_per_unit = round(b_path, 2)
-            total_bytes = agg["paths"] * b_path  # rank 0's paths over rank 0's busy time
+            bytes_per_unit = kernel_bytes_per_unit = FUSED_BYTES_PER_PATH[unit_mode]
+            total_bytes = agg["paths"] * bytes_per_unit  # rank 0's paths over rank 0's busy time
         else:
             bytes_per_unit, kernel_bytes_per_unit = ISECT_BYTES_PER_CAST, KERNEL_BYTES_PER_CAST
             total_bytes = agg["ray_casts"] * ISECT_BYTES_PER_CAST
         bytes_per_launch = total_bytes / launches
         busy_ms = agg["isect_busy_ms"]
         achieved = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+        equiv = None
+        if fused:
+            eq_gbs = agg["paths"] * b_path / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+            equiv = {"bytes_per_path": round(b_path, 1), "achieved": round(eq_gbs, 2),
+                     "frac": round(eq_gbs / HBM_PEAK_GBS, 5),
+                     "note": "SURVEY 8(d) whole-path bytes the wavefront would move for these paths, over the fused "
+                             "kernel's busy time; the fused kernel keeps them in registers"}
         per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         # whole-path bytes over the whole frame time, against the
         # spec peak and a stream-copy peak measured here (BASELINE.md plan)
@@ -471,7 +483,10 @@ def main():
             "pipeline_rule": "auto: fused for tiles of <= 32M paths, else wavefront (DESIGN.md §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
-                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "hw_queues": {"requested": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                                     "environment": HW_QUEUES_ENV,
+                                     "note": "GPU_MAX_HW_QUEUES set by bench.py for its own process (SPT_HW_QUEUES "
+                                             "overrides); the library sets none (DESIGN.md §6b)"},
                        "workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
@@ -481,8 +496,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",
-                         "basis": ("SURVEY 8(d) whole-path bytes of rank 0's paths / union of its fused launch "
-                                   "intervals") if fused else
+                         "basis": ("film bytes the fused kernel writes for rank 0's paths / union of its fused "
+                                   "launch intervals") if fused else
                                   "algorithmic bytes of all launches / union of their intervals (isect busy)",
                          "bytes_per_unit": bytes_per_unit, "kernel_bytes_per_unit": kernel_bytes_per_unit,
                          "unit_of_work": "path" if fused else "ray cast",
@@ -501,6 +516,7 @@ def main():
                          "pmc_note": pmc_note,
                          "build_id": build_id,
                          "valu": valu,
+                         "equivalent_wavefront": equiv,
                          "stream_copy_peak": round(copy_gbs, 1),
                          "path": {"bytes_per_path": round(b_path, 1),
                                   "formula": "84 + 120*S + 60*C (SURVEY 8d), S=%.4f C=%.4f" % (s_bar, c_bar),
@@ -517,16 +533,22 @@ def main():
             rec["wavefront_leg"] = wave_leg
         if args.save:
             np.save(args.save, image_main.cpu().numpy())
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
+            # rank 0 only, at any world size: the oracle on this host's cores,
+            # and the parity of the assembled image (every rank's tile,
+            # gathered) against that oracle render; the other ranks wait at
+            # the barrier below
             (orows, ofilm), rec["cpu_baseline"] = cpu_baseline(mesh, args, args.cpu_threads, kw, alb, emi)
             got = image_main[:, torch.as_tensor(orows, dtype=torch.long, device=dev), :].cpu().numpy()
             diff = got != ofilm
             rec["parity"] = {"rows": int(orows.size), "of_rows": H, "bitexact": bool(not diff.any()),
                              "values_differing": int(diff.sum()),
                              "max_abs_diff": float(np.abs(got - ofilm).max()) if got.size else 0.0,
+                             "image": "assembled from %d rank tile(s) by the gather" % world,
                              "against": "oracle/ (C restatement of main.cpp:354-446), the cpu_baseline render"}
         print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -413,6 +413,15 @@ spt_status spt_render_async(spt_scene scene, const spt_render_params* params, fl
                             uint64_t* ticket);
 spt_status spt_render_wait(spt_scene scene, uint64_t ticket, spt_render_stats* stats);
 
+/* The isect kernel's busy time across queued renders (a build addition, for the
+ * roofline: renders queued back to back overlap, so per-render busy times do
+ * not add up).  After _begin, every SPT_FLAG_TIMING render collected by
+ * spt_render_wait / spt_render contributes its isect launch intervals (the
+ * fused kernel's in the fused pipeline) on the scene's clock; _end returns the
+ * union of all of them in ms and the number of launches, and stops collecting. */
+spt_status spt_scene_isect_busy_begin(spt_scene scene);
+spt_status spt_scene_isect_busy_end(spt_scene scene, double* busy_ms, uint64_t* launches);
+
 /* Rows of tile `tile_index` (in increasing order).  Returns the row count;
  * writes at most `cap` row indices into rows (may be NULL). */
 uint32_t spt_tile_rows(uint32_t height, uint32_t tile_index, uint32_t tile_count,

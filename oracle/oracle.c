@@ -614,6 +614,18 @@ static inline void wray_setup(wray* r) {
     for (int k = 0; k < 3; k++) r->inv[k] = 1.0f / r->d[k];
 }
 
+#define BOX_PAD 1.000001f
+/* node culling runs 4e-6 below tmin (spt_math.h cull_tmin): a box culled there
+ * holds only triangles the box-exit rule drops anyway */
+#define CULL_TMIN_REL 4e-6f
+static inline float cull_tmin(float tmin) { return tmin - fabsf(tmin) * CULL_TMIN_REL; }
+static inline uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+/* max over the vertices of sign(d_k) * (v_k - o_k), sign(d_k) = sign(S) * sign(Sz) */
+static inline float exit_offset(float a, float b, float c, float S, float Sz) {
+    const int neg = ((fbits(S) ^ fbits(Sz)) >> 31) != 0u;
+    return neg ? -fminf(fminf(a, b), c) : fmaxf(fmaxf(a, b), c);
+}
+
 /* Returns 1 and t/u/v when the triangle is hit with t in [tmin, tmax]. */
 static inline int woop_test(const wray* r, const float* tv, float tmin, float tmax,
                             float* t_out, float* u_out, float* v_out) {
@@ -646,6 +658,10 @@ static inline int woop_test(const wray* r, const float* tv, float tmin, float tm
         B[k] = tv[3 + k] - r->o[k];
         C[k] = tv[6 + k] - r->o[k];
     }
+    /* the box-exit rule's farthest vertex offsets along the ray's motion in kx,
+     * ky (sign(d_k) = sign(S) * sign(Sz)); spt_math.h exit_offset */
+    const float ex = exit_offset(A[r->kx], B[r->kx], C[r->kx], r->Sx, r->Sz);
+    const float ey = exit_offset(A[r->ky], B[r->ky], C[r->ky], r->Sy, r->Sz);
     float Ax = A[r->kx] - r->Sx * A[r->kz], Ay = A[r->ky] - r->Sy * A[r->kz];
     float Bx = B[r->kx] - r->Sx * B[r->kz], By = B[r->ky] - r->Sy * B[r->kz];
     float Cx = C[r->kx] - r->Sx * C[r->kz], Cy = C[r->ky] - r->Sy * C[r->kz];
@@ -664,13 +680,19 @@ static inline int woop_test(const wray* r, const float* tv, float tmin, float tm
     float T = (U * Az + V * Bz) + W * Cz;
     float t = T / det;
     if (!(t >= tmin && t <= tmax)) return 0;
+    /* Box-exit rule (spt_math.h left_box_before_tmin): the hit counts only if
+     * the ray has not left the triangle's own box before tmin, so the closest
+     * hit does not depend on the tree (wavefront_isect.cu:103).
+     * Per axis the exit t times kBoxPad against tmin, without a divide. */
+    if (fmaxf(fmaxf(Az, Bz), Cz) * BOX_PAD < tmin) return 0;
+    if ((ex * fabsf(r->Sz)) * BOX_PAD < tmin * fabsf(r->Sx)) return 0;
+    if ((ey * fabsf(r->Sz)) * BOX_PAD < tmin * fabsf(r->Sy)) return 0;
     *t_out = t;
     *u_out = V / det;
     *v_out = W / det;
     return 1;
 }
 
-#define BOX_PAD 1.000001f
 /* Slab test over the closed box.  A direction component whose reciprocal is
  * infinite (d = +-0 or denormal) makes the ray parallel to that slab pair: it
  * is inside the slab for every t or never ((b - o) * inf would give NaN when
@@ -719,17 +741,9 @@ static void trace(const oscene* s, const wray* r, float tmin, float tmax, int cl
     while (sp) {
         const onode* nd = &s->nodes[stack[--sp]];
         /* the current hit padded like the exit planes: boxes entered at the
-         * hit's t (ties at shared edges / vertices) are still visited.  Boxes
-         * the ray leaves before tmin are culled, as on the GPU: a Woop hit a
-         * little past tmin outside its triangle's own box (origin on the
-         * triangle's plane) is then kept or not by the tree's box sizes
-         * (ORACLE_BOX_CULL_NEG_TMIN culls at -|tmin| and keeps it,
-         * like the brute-force scan) */
-#ifdef ORACLE_BOX_CULL_NEG_TMIN
-        if (!box_test(r, nd, fminf(tmin, -tmin), h->t * BOX_PAD)) continue;
-#else
-        if (!box_test(r, nd, tmin, h->t * BOX_PAD)) continue;
-#endif
+         * hit's t (ties at shared edges / vertices) are still visited; boxes
+         * the ray leaves before cull_tmin(tmin) are culled, as on the GPU */
+        if (!box_test(r, nd, cull_tmin(tmin), h->t * BOX_PAD)) continue;
         if (nd->count) {
             for (int32_t i = 0; i < nd->count; i++) {
                 consider(s, r, s->prims[nd->left + i], tmin, h);

@@ -197,6 +197,11 @@ struct Workspace {
     RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
     uint64_t next_ticket = 1;
     hipEvent_t epoch = nullptr;         // the first timed render's time origin: isect_begin/end_ms count from it
+    // spt_scene_isect_busy_begin/end: every isect launch interval (scene clock)
+    // of the renders collected in between, so the union across overlapping
+    // queued renders is exact (not one render's span less its overlap)
+    bool collect_iv = false;
+    std::vector<std::pair<double, double>> iv_all;
 
     void release() {
         for (WorkSet& w : sets) w.release();
@@ -208,6 +213,8 @@ struct Workspace {
             for (auto e : r.events) (void)hipEventDestroy(e);
             if (r.done) (void)hipEventDestroy(r.done);
         }
+        iv_all.clear();
+        collect_iv = false;
         const uint64_t t = next_ticket;  // tickets stay unique over the scene's life
         *this = Workspace();
         next_ticket = t;
@@ -412,7 +419,8 @@ spt_status render_slot(Workspace& ws, RenderSlot** out) {
 
 // Waits for a queued render and fills its statistics (device counters, the
 // union of its isect launch intervals, host wall time since it was queued).
-spt_status render_collect(RenderSlot& r, hipEvent_t epoch, spt_render_stats* out) {
+spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
+    const hipEvent_t epoch = ws.epoch;
     spt_render_stats rs = r.rs;
     r.pending = false;
     if (rs.tile_rows) {  // an empty tile queued nothing
@@ -459,6 +467,8 @@ spt_status render_collect(RenderSlot& r, hipEvent_t epoch, spt_render_stats* out
                 for (auto& x : iv) last = std::max(last, x.second);
                 rs.isect_begin_ms = (double)t_origin + iv[0].first;
                 rs.isect_end_ms = (double)t_origin + last;
+                if (ws.collect_iv)
+                    for (auto& x : iv) ws.iv_all.push_back({(double)t_origin + x.first, (double)t_origin + x.second});
             }
             float lo = 0.0f, hi = -1.0f;
             for (auto& x : iv) {
@@ -1747,6 +1757,25 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
     // the set's previous render (another stream, perhaps) must be done with it
     if (ws.used) HIP_TRY(hipStreamWaitEvent(stream, ws.free_ev, 0));
+    // From here on work is queued on the set's streams.  Any early return
+    // (a failed launch, a queue that did not drain) still joins the
+    // sub-wavefront streams into `stream` and records free_ev, so the next
+    // render that picks this set waits for whatever this one left running.
+    struct EnqueueGuard {
+        WorkSet& ws;
+        hipStream_t stream;
+        int K = 1;
+        bool armed = true;
+        ~EnqueueGuard() {
+            if (!armed) return;
+            for (int k = 1; k < K; k++) {
+                (void)hipEventRecord(ws.sub[k].join_ev, ws.sub[k].stream);
+                (void)hipStreamWaitEvent(stream, ws.sub[k].join_ev, 0);
+            }
+            (void)hipEventRecord(ws.free_ev, stream);
+            ws.used = true;
+        }
+    } guard{ws, stream, K};
     HIP_TRY(hipMemsetAsync(slot->dev, 0, sizeof(Stats), stream));
     // time origin for the isect launch intervals (their union = isect busy time)
     slot->timing = timing;
@@ -2020,6 +2049,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     HIP_TRY(hipEventRecord(slot->done, stream));
     HIP_TRY(hipEventRecord(ws.free_ev, stream));  // every sub-stream joined `stream` before the resolve
     ws.used = true;
+    guard.armed = false;
     rs.iterations = iters;
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
     rs.streams = (uint32_t)K;
@@ -2038,7 +2068,7 @@ spt_status spt_render_wait(spt_scene sc, uint64_t ticket, spt_render_stats* stat
     if (!r.pending || r.ticket != ticket)
         return fail(SPT_ERR_INVALID, "spt_render_wait: ticket %llu is not a queued render (already collected, "
                     "or %d renders were queued after it)", (unsigned long long)ticket, kRenderSlots);
-    return render_collect(r, sc->ws.epoch, stats_out);
+    return render_collect(r, sc->ws, stats_out);
 }
 
 spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev, spt_render_stats* stats_out,
@@ -2047,6 +2077,37 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
     spt_status st = spt_render_async(sc, pp, film_dev, stream, &ticket);
     if (st) return st;
     return spt_render_wait(sc, ticket, stats_out);
+}
+
+spt_status spt_scene_isect_busy_begin(spt_scene sc) {
+    if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_isect_busy_begin: NULL scene");
+    std::lock_guard<std::mutex> lock(sc->mu);
+    sc->ws.iv_all.clear();
+    sc->ws.collect_iv = true;
+    return SPT_OK;
+}
+
+spt_status spt_scene_isect_busy_end(spt_scene sc, double* busy_ms, uint64_t* launches) {
+    if (!sc || !busy_ms) return fail(SPT_ERR_INVALID, "spt_scene_isect_busy_end: NULL argument");
+    std::lock_guard<std::mutex> lock(sc->mu);
+    std::vector<std::pair<double, double>> iv;
+    iv.swap(sc->ws.iv_all);
+    sc->ws.collect_iv = false;
+    std::sort(iv.begin(), iv.end());
+    double busy = 0.0, lo = 0.0, hi = -1.0;
+    for (auto& x : iv) {
+        if (x.first > hi) {
+            if (hi > lo) busy += hi - lo;
+            lo = x.first;
+            hi = x.second;
+        } else {
+            hi = std::max(hi, x.second);
+        }
+    }
+    if (hi > lo) busy += hi - lo;
+    *busy_ms = busy;
+    if (launches) *launches = iv.size();
+    return SPT_OK;
 }
 
 }  // extern "C"

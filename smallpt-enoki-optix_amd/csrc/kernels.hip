@@ -181,18 +181,12 @@ __device__ __forceinline__ void slab(float p0, float p1, float o, float inv, flo
     t1 = (p1 - o) * inv;
 }
 
-// Box culling lower bound (tbox).  Default: boxes the ray leaves before tmin
-// are culled.  A ray leaving a surface (origin on a triangle's plane) can get
-// a Woop hit a little past tmin that lies outside the triangle's own box (the
-// t of a near-coplanar origin is all rounding); whether a tree keeps it then
-// depends on how tight its boxes are.  SPT_BOX_CULL_TMIN=0
-// culls at -|tmin| instead and keeps such hits like a brute-force scan, at
-// -12 % on config 1 and -3.5 % on config 4 (profiles/r03_parity/), so it is
-// an experiment, not the default.
-#ifndef SPT_BOX_CULL_TMIN
-#define SPT_BOX_CULL_TMIN 1
-#endif
-__device__ __forceinline__ float box_tmin(float tmin) { return SPT_BOX_CULL_TMIN ? tmin : fminf(tmin, -tmin); }
+// Box culling lower bound (tbox): boxes the ray leaves before cull_tmin(tmin),
+// 4e-6 below tmin, are culled.  With the box-exit rule of the triangle test
+// (spt_math.h left_box_before_tmin) every triangle under such a box that the
+// Woop test would accept past tmin is dropped by the rule too, so the closest
+// hit does not depend on the tree's box sizes.
+__device__ __forceinline__ float box_tmin(float tmin) { return cull_tmin(tmin); }
 
 struct Tracer {
     static constexpr int kMinWaves = 1;

@@ -202,19 +202,58 @@ SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     return r;
 }
 
-// The sheared, permuted vertices (Woop et al. 2013 §3).
+// The sheared, permuted vertices (Woop et al. 2013 §3), and for the box-exit
+// rule below the triangle's farthest vertex offset along the ray's motion in
+// kx and in ky (ex, ey: max of sign(d_k) * (v_k - o_k) over the vertices).
 struct WoopShear {
     float Akz, Bkz, Ckz, Ax, Ay, Bx, By, Cx, Cy;
+    float ex, ey;
 };
+// sign(d_kx) = sign(Sx) * sign(Sz), so the direction itself need not be kept
+SPT_HD float exit_offset(float a, float b, float c, float S, float Sz) {
+    const bool neg = ((f2u(S) ^ f2u(Sz)) >> 31) != 0u;
+    return neg ? -fminf(fminf(a, b), c) : fmaxf(fmaxf(a, b), c);
+}
 SPT_HD WoopShear woop_shear(const WoopRay& r, V3 p0, V3 p1, V3 p2) {
     V3 A = p0 - r.o, B = p1 - r.o, C = p2 - r.o;
     const int kx = r.kx(), ky = r.ky(), kz = r.kz();
     WoopShear w;
     w.Akz = comp(A, kz); w.Bkz = comp(B, kz); w.Ckz = comp(C, kz);
-    w.Ax = comp(A, kx) - r.Sx * w.Akz; w.Ay = comp(A, ky) - r.Sy * w.Akz;
-    w.Bx = comp(B, kx) - r.Sx * w.Bkz; w.By = comp(B, ky) - r.Sy * w.Bkz;
-    w.Cx = comp(C, kx) - r.Sx * w.Ckz; w.Cy = comp(C, ky) - r.Sy * w.Ckz;
+    const float Akx = comp(A, kx), Bkx = comp(B, kx), Ckx = comp(C, kx);
+    const float Aky = comp(A, ky), Bky = comp(B, ky), Cky = comp(C, ky);
+    w.ex = exit_offset(Akx, Bkx, Ckx, r.Sx, r.Sz);
+    w.ey = exit_offset(Aky, Bky, Cky, r.Sy, r.Sz);
+    w.Ax = Akx - r.Sx * w.Akz; w.Ay = Aky - r.Sy * w.Akz;
+    w.Bx = Bkx - r.Sx * w.Bkz; w.By = Bky - r.Sy * w.Bkz;
+    w.Cx = Ckx - r.Sx * w.Ckz; w.Cy = Cky - r.Sy * w.Ckz;
     return w;
+}
+
+// Box-exit rule: a hit is kept only if the ray has not left the triangle's
+// own bounding box before tmin.  Exactly, a point of the triangle lies in its
+// box, so a ray that left the box before tmin cannot meet the triangle at
+// t >= tmin; a Woop t just past tmin there is rounding (the origin on or next
+// to the triangle's plane).  Without the rule such a hit is kept or not
+// depending on whether the tree's boxes around it are culled at tmin (a tight
+// box drops it, a loose one keeps it: DESIGN.md §2), so the closest hit would
+// depend on the acceleration structure, which wavefront_isect.cu:103 does not
+// allow.  Per axis k the exit is E_k = (farthest vertex offset) / |d_k|:
+//   kz: E = max(Az, Bz, Cz)  (Az = Sz (v_kz - o_kz) is already in t units),
+//   kx: E = ex |Sz| / |Sx|   (|d_kx| = |Sx| / |Sz|), ky likewise,
+// tested as E * kBoxPad < tmin without a divide.  Each side has <= 4 ulps of
+// rounding, under kBoxPad's 8.4, so a hit whose exact box exit is >= tmin is
+// never dropped; and node culling runs at cull_tmin() (4e-6 below tmin) so a
+// box the tree culls holds only triangles this rule drops anyway.
+#ifndef SPT_TRI_BOX_RULE
+#define SPT_TRI_BOX_RULE 1
+#endif
+constexpr float kCullTminRel = 4e-6f;
+SPT_HD float cull_tmin(float tmin) { return tmin - fabsf(tmin) * kCullTminRel; }
+SPT_HD bool left_box_before_tmin(const WoopRay& r, const WoopShear& w, float Az, float Bz, float Cz, float tmin) {
+    if (fmaxf(fmaxf(Az, Bz), Cz) * kBoxPad < tmin) return true;
+    const float asz = fabsf(r.Sz);
+    if ((w.ex * asz) * kBoxPad < tmin * fabsf(r.Sx)) return true;
+    return (w.ey * asz) * kBoxPad < tmin * fabsf(r.Sy);
 }
 
 struct NoReload {  // the vertices stay in registers (host)
@@ -263,6 +302,9 @@ SPT_HD bool woop_test_raw(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, 
     float T = (U * Az + V * Bz) + W * Cz;
     float t = T / det;
     if (!(t >= tmin && t <= tmax)) return false;
+#if SPT_TRI_BOX_RULE
+    if (left_box_before_tmin(r, w, Az, Bz, Cz, tmin)) return false;
+#endif
     t_out = t;
     V_out = V;
     W_out = W;

@@ -35,6 +35,7 @@ EXPORTED = [
     "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
     "spt_bvh_build_stats", "spt_scene_set_texture", "spt_scene_set_spheres", "spt_scene_set_material_kinds",
     "spt_scene_save", "spt_scene_load", "spt_scene_cache_info",
+    "spt_scene_isect_busy_begin", "spt_scene_isect_busy_end",
 ]
 SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
@@ -162,6 +163,8 @@ def _load() -> ctypes.CDLL:
         "spt_render": (i32, [vp, POINTER(RenderParams), vp, POINTER(RenderStats), vp]),
         "spt_render_async": (i32, [vp, POINTER(RenderParams), vp, vp, POINTER(u64)]),
         "spt_render_wait": (i32, [vp, u64, POINTER(RenderStats)]),
+        "spt_scene_isect_busy_begin": (i32, [vp]),
+        "spt_scene_isect_busy_end": (i32, [vp, POINTER(ctypes.c_double), POINTER(u64)]),
         "spt_tile_rows": (u32, [u32, u32, u32, u32, vp, u32]),
         "spt_default_params": (None, [POINTER(RenderParams)]),
         "spt_last_error": (c_char_p, []),

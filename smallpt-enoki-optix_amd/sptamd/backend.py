@@ -16,7 +16,7 @@ import ctypes
 import math
 import os
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -408,6 +408,18 @@ class Scene:
         st = RenderStats()
         check(lib.spt_render_wait(self.backend.handle, ticket, ctypes.byref(st)), "spt_render_wait")
         return st.as_dict()
+
+    def isect_busy_begin(self) -> None:
+        """spt_scene_isect_busy_begin: start collecting isect launch intervals."""
+        check(lib.spt_scene_isect_busy_begin(self.backend.handle), "spt_scene_isect_busy_begin")
+
+    def isect_busy_end(self) -> Tuple[float, int]:
+        """spt_scene_isect_busy_end: (union of the intervals collected since
+        isect_busy_begin in ms, launches) across every render collected."""
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        check(lib.spt_scene_isect_busy_end(self.backend.handle, ctypes.byref(ms), ctypes.byref(n)),
+              "spt_scene_isect_busy_end")
+        return ms.value, n.value
 
     def _film(self, params: RenderParams, film: Optional[torch.Tensor]) -> torch.Tensor:
         rows = _lib.tile_row_count(params.height, params.tile_index, params.tile_count, params.rows_per_group)

@@ -31,10 +31,13 @@ class TileGather:
         self.tile = self.tiles[0]
         self.gather_list: Optional[List[torch.Tensor]] = None
         self.image: Optional[torch.Tensor] = None
+        # the collective runs whenever a process group exists (at world size
+        # 1 too: one rank's RCCL gather), else one process copies its tile
+        self.collective = world > 1 or (dist.is_available() and dist.is_initialized())
         if rank == 0:
             self.image = torch.zeros((3, height, width), dtype=torch.float32, device=device)
             self.row_index = [torch.as_tensor(r, dtype=torch.long, device=device) for r in self.rows]
-            if world > 1:
+            if self.collective:
                 self.gather_list = [torch.empty_like(self.tile) for _ in range(world)]
 
     @property
@@ -51,7 +54,7 @@ class TileGather:
         """Collective: every rank calls it; rank 0 gets the assembled image
         from every rank's film buffer k (on the current stream)."""
         tile = self.tiles[k]
-        if self.world == 1:
+        if not self.collective:
             self.image.copy_(self.tile_view(k))
             return self.image
         if tile.is_cuda and dist.get_backend() != "nccl":

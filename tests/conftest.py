@@ -46,3 +46,27 @@ def spaced_rows(height, n):
     """n evenly spaced rows of [0, height) (first and last included)."""
     import numpy as np
     return np.unique(np.linspace(0, height - 1, n).round().astype(np.int32))
+
+
+def surface_rays(intersect, lo, hi, n, seed):
+    """Rays that leave surfaces, as a path's bounces do (the case where the
+    closest hit could depend on the tree: an origin on or next to a
+    triangle's plane).  Primary rays from random points of the
+    box [lo, hi] in random directions are cast with `intersect(o, d) -> (tri,
+    t, u, v)`; each hit point o + t d (float32, as shade computes it,
+    optix_backend.h:469) starts a new ray in a random direction or toward a random point of the box.  Returns the
+    secondary rays' (o, d), (3, m) float32 each."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lo, hi = np.asarray(lo, np.float32), np.asarray(hi, np.float32)
+    o = (lo[:, None] + (hi - lo)[:, None] * rng.random((3, n))).astype(np.float32)
+    d = rng.normal(size=(3, n)).astype(np.float32)
+    tri, t, _, _ = intersect(o, d)
+    h = tri >= 0
+    o, d, t = o[:, h], d[:, h], t[h]
+    p = (o + t[None, :] * d).astype(np.float32)
+    # half in uniform random directions, half toward random points of the box
+    # (more of those meet geometry again)
+    tgt = lo[:, None] + (hi - lo)[:, None] * rng.random(p.shape)
+    d2 = np.where(np.arange(p.shape[1]) % 2 == 0, rng.normal(size=p.shape), tgt - p).astype(np.float32)
+    return p, d2

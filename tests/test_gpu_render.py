@@ -126,18 +126,8 @@ def test_env_radiance(gscene, oscene):
     np.testing.assert_array_equal(got, ref)
 
 
-def test_headline_config_whole_image(gscene, oscene):
-    """BASELINE configs[1] shape (1024^2 x 64 spp, depth 8), both pipelines:
-    the WHOLE image bit-equal to the oracle's (67M paths on the host), the
-    same number of rays traced, and the device's work accounting complete."""
-    w = h = 1024
-    spp, depth = 64, 8
-    got, st = gpu_render(gscene, w, h, spp, depth)
-    assert got.shape == (3, h, w)
-    ref, casts = oracle_render(oscene, w, h, spp, depth, nthreads=16)
-    np.testing.assert_array_equal(got, ref)
-    assert st["ray_casts"] == casts
-    assert st["paths"] == w * h * spp
+# BASELINE configs[1] itself (the bench's 231k-triangle scene, whole image,
+# both pipelines): tests/test_gpu_configs.py::test_config1_headline_whole_image
 
 
 def test_gpu_matches_committed_golden():

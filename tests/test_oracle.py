@@ -174,6 +174,23 @@ def test_bvh_equals_bruteforce():
     assert (a[0] >= 0).sum() > 1000
 
 
+def test_bvh_equals_bruteforce_on_surface_leaving_rays():
+    """Tree independence where it is at stake: rays leaving the surfaces they
+    hit (origins on or next to triangle planes, both hemispheres), BVH2 =
+    brute force bit for bit, with the box-exit rule."""
+    from conftest import surface_rays
+    mesh = scenes.mitsuba_synth(detail=0.25)
+    bvh = O.OracleScene(mesh, use_bvh=True)
+    brute = O.OracleScene(mesh, use_bvh=False)
+    pos = np.asarray(mesh["pos"], np.float32)
+    o, d = surface_rays(lambda o, d: bvh.intersect(o, d), pos.min(0), pos.max(0), 24000, seed=11)
+    a = bvh.intersect(o, d)
+    b = brute.intersect(o, d)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+    assert o.shape[1] > 8000 and (a[0] >= 0).sum() > 500
+
+
 def test_golden_vectors():
     g = np.load(GOLDEN)
     for s, row in zip(g["pcg_seeds"], g["pcg_u32"]):
@@ -397,13 +414,14 @@ def test_glass_sphere_conserves_energy():
 
 
 def test_hit_past_tmin_outside_triangle_box_known_case():
-    """Pinned known case (config 4's city_synth, found by tools/diag_parity.py):
-    a ray leaving a column surface, its origin on the triangle's plane, gets a
-    Woop hit at t = 0.0015 (past tmin = 0.001) outside the triangle's own box,
-    which the ray leaves at t = 0.0003.  Brute force keeps the hit; a tree
-    that culls boxes left before tmin (the oracle's tight BVH2, the GPU's
-    default) drops it, while a looser box (the GPU's quantised BVH8 in the
-    full scene) keeps it: one sample of 10.5M paths differed."""
+    """Pinned known case (config 4's city_synth, found by tools/diag_parity.py in
+    round 3): a ray leaving a column surface, its origin on the triangle's
+    plane, gets a Woop hit at t = 0.0015 (past tmin = 0.001) outside the
+    triangle's own box, which the ray leaves at t = 0.0003 (in x and z).
+    Without the box-exit rule brute force kept the hit and a tree that culls
+    boxes left before tmin dropped it, so the answer depended on the tree.
+    With the rule (spt_math.h left_box_before_tmin, oracle.c woop_test) the
+    hit is dropped by every tracer: brute force and BVH agree on a miss."""
     pos = np.array([[-0.249440879, -1, 8.8333292], [-0.212132037, 5, 8.78786755], [-0.249440879, 5, 8.8333292]],
                    np.float32)
     m = {"pos_tri": np.array([[0, 1, 2]], np.int32), "pos": pos}
@@ -411,5 +429,38 @@ def test_hit_past_tmin_outside_triangle_box_known_case():
     d = np.array([[-0.3425644636154175], [0.8412052392959595], [0.4182586371898651]], np.float32)
     brute = O.OracleScene(m, use_bvh=False).intersect(o, d)
     bvh = O.OracleScene(m).intersect(o, d)
-    assert brute[0][0] == 0 and abs(float(brute[1][0]) - 0.0015052289) < 1e-9
+    assert brute[0][0] == -1
     assert bvh[0][0] == -1
+    # the same ray from just behind the plane's neighbourhood (tmin 0) hits:
+    # the rule only drops hits whose box the ray has left before tmin
+    t0 = np.zeros(1, np.float32)
+    hit0 = O.OracleScene(m, use_bvh=False).intersect(o, d, tmin=t0)
+    assert hit0[0][0] == 0
+
+
+def test_box_exit_rule_keeps_hits_on_axis_aligned_triangles():
+    """The rule must not drop genuine hits where the Woop t and the slab t
+    round differently: axis-aligned walls hit head-on, at grazing angles and
+    close to tmin, BVH = brute force, every ray that crosses the wall inside
+    its extent beyond tmin hits it."""
+    rng = np.random.default_rng(7)
+    # a wall x = 1 (two triangles over y, z in [-1, 1]) and a floor y = 0
+    pos = np.array([[1, -1, -1], [1, 1, -1], [1, 1, 1], [1, -1, 1],
+                    [-3, 0, -3], [3, 0, -3], [3, 0, 3], [-3, 0, 3]], np.float32)
+    tri = np.array([[0, 1, 2], [0, 2, 3], [4, 5, 6], [4, 6, 7]], np.int32)
+    m = {"pos_tri": tri, "pos": pos}
+    n = 20000
+    o = np.stack([rng.uniform(-0.5, 0.999, n), rng.uniform(0.0005, 0.9, n), rng.uniform(-0.9, 0.9, n)]).astype(np.float32)
+    d = np.stack([rng.uniform(0.01, 1, n), rng.uniform(-1, 1, n), rng.uniform(-1, 1, n)]).astype(np.float32)
+    brute = O.OracleScene(m, use_bvh=False).intersect(o, d)
+    bvh = O.OracleScene(m).intersect(o, d)
+    for a, b in zip(brute, bvh):
+        np.testing.assert_array_equal(a, b)
+    # float64 ground truth for the wall: t = (1 - ox) / dx, point inside the square
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    tw = (1.0 - o64[0]) / d64[0]
+    yw, zw = o64[1] + tw * d64[1], o64[2] + tw * d64[2]
+    tf = np.where(d64[1] < 0, -o64[1] / np.where(d64[1] < 0, d64[1], -1), np.inf)  # floor first?
+    clear = (np.abs(yw) < 0.999) & (np.abs(zw) < 0.999) & (tw > 0.0011) & (tw < tf * 0.999)
+    assert clear.sum() > 1000
+    assert np.all(np.isin(brute[0][clear], [0, 1])), "a clear wall hit was dropped"
