@@ -75,6 +75,16 @@ class Scene {
     void render(const spt_render_params& p, float* film_dev, spt_render_stats* stats, void* stream = nullptr) {
         check(spt_render(scene_, &p, film_dev, stats, stream), "spt_render");
     }
+    // Commit a mesh loaded elsewhere (read only: several devices' scenes may
+    // be built from one host mesh, one thread per device).
+    void commit_from(const Mesh& mesh, int device) {
+        check(spt_init(device), "spt_init");
+        const spt_mesh& m = mesh.m;
+        check(spt_scene_create(m.pos_tri, m.pos, m.nvert, m.ntri, m.nrm_tri, m.nrm, m.nnrm, m.tc_tri, m.tc, m.ntc,
+                               m.mat_id, &scene_),
+              "spt_scene_create");
+        pbrt_ = mesh.pbrt;
+    }
     spt_scene handle() const { return scene_; }
     const spt_mesh& mesh() const { return mesh_->m; }  // not after load()
     const spt_pbrt_info& pbrt_info() const { return pbrt_; }

@@ -211,6 +211,8 @@ struct WoopShear {
 };
 // sign(d_kx) = sign(Sx) * sign(Sz), so the direction itself need not be kept
 SPT_HD float exit_offset(float a, float b, float c, float S, float Sz) {
+    // (a branch-free select of both maxima, or an xor of the sign bits, made
+    // the isect kernel spill at its 64-VGPR budget; this form does not)
     const bool neg = ((f2u(S) ^ f2u(Sz)) >> 31) != 0u;
     return neg ? -fminf(fminf(a, b), c) : fmaxf(fmaxf(a, b), c);
 }
