@@ -493,8 +493,12 @@ spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
 // of X's inner children (level L + 1 <= depth), and the stack then holds one
 // group per node on the path root..X: at most depth - 1 entries.  A tight
 // stack is LDS, and LDS sets the occupancy (spt_config.stack_slack adds entries).
+#ifndef SPT_STACK_CAP
+#define SPT_STACK_CAP 0  // experiment only (no overflow handling): cap the LDS stack entries
+#endif
 uint32_t bvh8_stack_entries(uint32_t depth, uint32_t slack) {
-    return std::max<uint32_t>(1, depth > 1 ? depth - 1 + slack : 1 + slack);
+    const uint32_t n = std::max<uint32_t>(1, depth > 1 ? depth - 1 + slack : 1 + slack);
+    return SPT_STACK_CAP ? std::min<uint32_t>(n, SPT_STACK_CAP) : n;
 }
 
 // Range checks of spt_scene_set_config / spt_scene_create_cfg.
