@@ -774,11 +774,7 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
         const uint32_t t = slot2tri[s];
         h_o2s[t] = (int32_t)s;
         const float* v = &tv[(size_t)t * 9];
-        for (int k = 0; k < 3; k++) {
-            float w = 0.0f;
-            if (k == 0) { uint32_t id = t; std::memcpy(&w, &id, 4); }
-            h_tris[s * kTriQuads + k] = make_float4(v[k * 3], v[k * 3 + 1], v[k * 3 + 2], w);
-        }
+        tri_record_fill((float*)&h_tris[s * kTriQuads], v, t);
         // Geometric normal fallback for a missing vertex normal (index -1).
         V3 g = normalize(cross(v3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), v3(v[6] - v[0], v[7] - v[1], v[8] - v[2])));
         int32_t mat = mat_id ? mat_id[t] : 0;
@@ -1083,7 +1079,7 @@ spt_status spt_scene_destroy(spt_scene sc) {
 namespace {
 
 constexpr char kCacheMagic[8] = {'S', 'P', 'T', 'S', 'C', 'E', 'N', 'E'};
-constexpr uint32_t kCacheVersion = 1;
+constexpr uint32_t kCacheVersion = 2;  // 2: 64-B rotated triangle records (spt_internal.h)
 constexpr size_t kCacheChunk = size_t(64) << 20;  // host staging per read / write / download
 
 // Sections, in file order.
@@ -1327,7 +1323,7 @@ spt_status cache_check_nodes(const char* path, const char* what, const CacheHead
 }
 
 // Index arrays of a loaded scene: orig2slot maps into the slots, every slot's
-// original id (v0.w) lies in [0, ntri), material kinds are SPT_MAT_*.
+// original id (float 15 of its record) lies in [0, ntri), material kinds are SPT_MAT_*.
 spt_status cache_check_indices(const char* path, const char* what, const CacheHeader& h, uint32_t s,
                                const std::vector<uint8_t>& buf) {
     const uint64_t nt = h.ntri;
@@ -1340,9 +1336,9 @@ spt_status cache_check_indices(const char* path, const char* what, const CacheHe
     } else if (s == kSecTris) {
         const uint32_t* t = (const uint32_t*)buf.data();
         for (uint64_t i = 0; i < nt; i++)
-            if (t[i * kTriQuads * 4 + 3] >= nt)
+            if (t[i * kTriFloats + kTriIdFloat] >= nt)
                 return fail(SPT_ERR_INVALID, "%s: %s: triangle slot %llu has id %u", what, path, (unsigned long long)i,
-                            t[i * kTriQuads * 4 + 3]);
+                            t[i * kTriFloats + kTriIdFloat]);
     } else if (s == kSecKinds) {
         const uint32_t* k = (const uint32_t*)buf.data();
         for (uint32_t i = 0; i < h.nkind; i++)

@@ -982,8 +982,10 @@ __global__ __launch_bounds__(kBlock) void scene_slots_kernel(DeviceMeshIn m, con
     const uint32_t t = slot2tri[sl];
     o2s[t] = (int32_t)sl;
     const float* v = tv + (size_t)t * 9;
-    for (int k = 0; k < 3; k++)
-        tris[(size_t)sl * kTriQuads + k] = make_float4(v[k * 3], v[k * 3 + 1], v[k * 3 + 2], k == 0 ? u2f(t) : 0.0f);
+    float rec[kTriFloats];
+    tri_record_fill(rec, v, t);
+    for (int k = 0; k < 4; k++)
+        tris[(size_t)sl * kTriQuads + k] = make_float4(rec[4 * k], rec[4 * k + 1], rec[4 * k + 2], rec[4 * k + 3]);
     // geometric normal fallback for a missing vertex normal (as spt_scene_create's host loop)
     const V3 g = normalize(cross(v3(v[3] - v[0], v[4] - v[1], v[5] - v[2]), v3(v[6] - v[0], v[7] - v[1], v[8] - v[2])));
     const int32_t mat = m.mat_id ? m.mat_id[t] : 0;

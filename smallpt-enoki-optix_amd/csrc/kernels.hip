@@ -78,14 +78,26 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #endif
 
 // ------------------------------------------------------------- traversal
+// Triangle records (spt_internal.h): vertex i of slot s rotated by r starts at
+// float 5 i + r, the original id is float 15.
+__device__ __forceinline__ const float* tri_rec(const DeviceScene& sc, uint32_t s) {
+    return (const float*)sc.tris + (size_t)s * kTriFloats;
+}
+__device__ __forceinline__ uint32_t tri_id(const DeviceScene& sc, uint32_t s) { return f2u(tri_rec(sc, s)[kTriIdFloat]); }
+__device__ __forceinline__ void tri_vertices(const float* f, V3& a, V3& b, V3& c) {
+    a = v3(f[0], f[1], f[2]);
+    b = v3(f[5], f[6], f[7]);
+    c = v3(f[10], f[11], f[12]);
+}
+
 // woop_test's double-precision fallback re-reads the triangle (rare path) so
-// the single-precision path need not keep the sheared vertices live.
+// the single-precision path need not keep the sheared vertices live; f points
+// at the record plus the lane's rotation.
 struct TriReload {
-    const float4* tp;
+    const float* f;
     __device__ __forceinline__ void operator()(V3& a, V3& b, V3& c) const {
-        const float* f = (const float*)tp;
-        const auto ld = [f](int i) { return __builtin_nontemporal_load(f + i); };
-        a = v3(ld(0), ld(1), ld(2)); b = v3(ld(4), ld(5), ld(6)); c = v3(ld(8), ld(9), ld(10));
+        const auto ld = [this](int i) { return __builtin_nontemporal_load(f + i); };
+        a = v3(ld(0), ld(1), ld(2)); b = v3(ld(5), ld(6), ld(7)); c = v3(ld(10), ld(11), ld(12));
     }
 };
 
@@ -267,10 +279,12 @@ struct Tracer {
         for (uint32_t i = 0; i < cnt; i++) {
             stats.tri();
             const uint32_t s = first + i;
-            const float4 t0 = sc.tris[(size_t)s * kTriQuads], t1 = sc.tris[(size_t)s * kTriQuads + 1], t2 = sc.tris[(size_t)s * kTriQuads + 2];
+            const float* f = tri_rec(sc, s);
+            V3 p0, p1, p2;
+            tri_vertices(f, p0, p1, p2);  // world order (rotation 0)
             float t, u, v;
-            if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z), TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, u, v)) {
-                const uint32_t id = f2u(t0.w);
+            if (woop_test(wr, p0, p1, p2, TriReload{f}, tmin, h.t, t, u, v)) {
+                const uint32_t id = f2u(f[kTriIdFloat]);
                 if (t < h.t || id < h.id) {
                     h.t = t;
                     h.id = id;
@@ -331,7 +345,10 @@ struct Tracer8T {
     WoopRay wr;
     V3 o;
     float ix, iy, iz, tmin, tbox;
-    uint32_t oct_rep;  // the ray's inverted octant (0..7) replicated in every byte
+    // the ray's inverted octant (0..7) replicated in every byte; bits 3-4 of the
+    // low byte hold the triangle-record rotation (0..2) of the ray's dominant
+    // axis (the octant users mask each byte to its low 3 bits)
+    uint32_t oct_rep;
     // node group: unvisited hit children in bits 24..31 (bit 24 + (slot ^
     // octant)), the child-group word in bits 0..23 (child s of a node sits at
     // (word << group_shift) + s, gpu_bvh8_holes) — one word, also one LDS stack entry
@@ -354,25 +371,32 @@ struct Tracer8T {
     __device__ __forceinline__ uint4* hrec(const DeviceScene& sc, const Lds& L) const {
         return wrec(sc, L) + kIsectBlock;
     }
-    // The LDS hit record: (slot, id, u, v); with kDefer (slot, V, W, det),
-    // u = V / det and v = W / det divided once for the hit the ray keeps and
-    // the original id read back from the triangle record.
+    // The LDS hit record: (slot, -, u, v); with kDefer (slot, V, W, det),
+    // u = V / det and v = W / det divided once for the hit the ray keeps.  The
+    // original id is read back from the triangle record (the isect queue
+    // kernel writes the slot and never asks for it).
     __device__ __forceinline__ TraceHit hit(const DeviceScene& sc, const Lds& L) const {
         if constexpr (!kLds) return h;
         const uint4 r = *hrec(sc, L);
         TraceHit x;
         x.slot = (int32_t)r.x;
         x.t = h.t;
-        if constexpr (!kDefer) {
-            x.id = r.y; x.u = u2f(r.z); x.v = u2f(r.w);
-        } else if (r.x == 0xffffffffu) {
+        if (r.x == 0xffffffffu) {
             x.id = 0xffffffffu; x.u = 0.0f; x.v = 0.0f;
+        } else if constexpr (!kDefer) {
+            x.id = tri_id(sc, r.x); x.u = u2f(r.z); x.v = u2f(r.w);
         } else {
-            x.id = f2u(sc.tris[(size_t)r.x * kTriQuads].w);
+            x.id = tri_id(sc, r.x);
             x.u = u2f(r.y) / u2f(r.w);
             x.v = u2f(r.z) / u2f(r.w);
         }
         return x;
+    }
+    __device__ __forceinline__ uint32_t rot() const { return (oct_rep >> 3) & 3u; }
+    // the origin in the rotated records' (kx, ky, kz) order
+    __device__ __forceinline__ V3 rot_origin() const {
+        const uint32_t r = rot();
+        return r == 0 ? o : (r == 1 ? v3(o.y, o.z, o.x) : v3(o.z, o.x, o.y));
     }
 
     __device__ __forceinline__ void init(const DeviceScene& sc, V3 o_, V3 d, float tmin_, float tmax_, bool anyhit_,
@@ -397,7 +421,8 @@ struct Tracer8T {
         ix = __builtin_amdgcn_rcpf(dx); iy = __builtin_amdgcn_rcpf(dy); iz = __builtin_amdgcn_rcpf(dz);
         const uint32_t oct = (ix < 0.0f ? 1u : 0u) | (iy < 0.0f ? 2u : 0u) | (iz < 0.0f ? 4u : 0u);
         const uint32_t oct_inv = oct ^ 7u;
-        oct_rep = oct_inv * 0x01010101u;
+        const uint32_t kz = wr.k >> 4;  // rotation r = (kz + 1) mod 3 puts kz last
+        oct_rep = oct_inv * 0x01010101u | ((kz == 2u ? 0u : kz + 1u) << 3);
         tmin = tmin_;
         tbox = box_tmin(tmin_);
         anyhit = anyhit_;
@@ -520,36 +545,40 @@ struct Tracer8T {
         take_hits(hm, w1.x, w1.y);
     }
 
-    __device__ __forceinline__ bool tri_test(const DeviceScene& sc, const float4 t0, const float4 t1, const float4 t2,
-                                             uint32_t s, const Lds& L, const uint4 wk) {
+    // P0..P2: the slot's vertices loaded rotated by rot() (f: the record + rot)
+    __device__ __forceinline__ bool tri_test(const DeviceScene& sc, V3 P0, V3 P1, V3 P2, const float* f, uint32_t s,
+                                             const Lds& L, const uint4 wk) {
         float t, u, v;
+        WoopRay wl;
+        wl.o = o;
+        if constexpr (kLds) { wl.Sx = u2f(wk.x); wl.Sy = u2f(wk.y); wl.Sz = u2f(wk.z); wl.k = wk.w; }
+        else wl = wr;
+        const V3 O = rot_origin();
         if constexpr (kLds) {
-            WoopRay wl;
-            wl.o = o; wl.Sx = u2f(wk.x); wl.Sy = u2f(wk.y); wl.Sz = u2f(wk.z); wl.k = wk.w;
+            uint4* hr = hrec(sc, L);
             if constexpr (!kDefer) {
-                if (woop_test(wl, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                              TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, u, v)) {
-                    // accepted means t <= h.t; a tie goes to the smaller original id
-                    const uint32_t id = f2u(t0.w);
-                    uint4* hr = hrec(sc, L);
-                    if (t < h.t || id < hr->y) {
+                if (woop_test_rot(wl, O, P0, P1, P2, TriReload{f}, tmin, h.t, t, u, v)) {
+                    // accepted means t <= h.t; a tie goes to the smaller original
+                    // id (both read from the triangle records: rare)
+                    bool take = t < h.t;
+                    if (!take) {
+                        const uint32_t cs = hr->x;
+                        take = cs == 0xffffffffu || tri_id(sc, s) < tri_id(sc, cs);
+                    }
+                    if (take) {
                         h.t = t;
-                        *hr = make_uint4((uint32_t)s, id, f2u(u), f2u(v));
+                        *hr = make_uint4((uint32_t)s, 0u, f2u(u), f2u(v));
                     }
                     return true;
                 }
                 return false;
             }
             float V, W, det;
-            if (woop_test_raw(wl, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                              TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, V, W, det)) {
-                // accepted means t <= h.t; a tie goes to the smaller original
-                // id (the kept hit's id read back from its triangle: rare)
-                uint4* hr = hrec(sc, L);
+            if (woop_test_raw_rot(wl, O, P0, P1, P2, TriReload{f}, tmin, h.t, t, V, W, det)) {
                 bool take = t < h.t;
                 if (!take) {
                     const uint32_t cs = hr->x;
-                    take = cs == 0xffffffffu || f2u(t0.w) < f2u(sc.tris[(size_t)cs * kTriQuads].w);
+                    take = cs == 0xffffffffu || tri_id(sc, s) < tri_id(sc, cs);
                 }
                 if (take) {
                     h.t = t;
@@ -559,9 +588,8 @@ struct Tracer8T {
             }
             return false;
         }
-        if (woop_test(wr, v3(t0.x, t0.y, t0.z), v3(t1.x, t1.y, t1.z), v3(t2.x, t2.y, t2.z),
-                      TriReload{sc.tris + (size_t)s * kTriQuads}, tmin, h.t, t, u, v)) {
-            const uint32_t id = f2u(t0.w);
+        if (woop_test_rot(wl, O, P0, P1, P2, TriReload{f}, tmin, h.t, t, u, v)) {
+            const uint32_t id = tri_id(sc, s);
             if (t < h.t || id < h.id) {
                 h.t = t;
                 h.id = id;
@@ -605,7 +633,9 @@ struct Tracer8T {
         const uint32_t s = has_tri ? tbase + (uint32_t)__builtin_ctz(thits) : 0u;
         if (has_tri) stats.tri();
         thits &= thits - 1u;
-        const float4 t0 = sc.tris[(size_t)s * kTriQuads], t1 = sc.tris[(size_t)s * kTriQuads + 1], t2 = sc.tris[(size_t)s * kTriQuads + 2];
+        const float* f = tri_rec(sc, s) + rot();
+        V3 P0, P1, P2;
+        tri_vertices(f, P0, P1, P2);
         uint4 wk = make_uint4(0u, 0u, 0u, 0u);
         if constexpr (kLds) wk = *wrec(sc, L);
         if (do_node && !(nhits & 0xff000000u)) {
@@ -629,7 +659,7 @@ struct Tracer8T {
         const uint4 w0 = np[0], w1 = np[1], w2 = np[2], w3 = np[3];
         uint4 w4 = w3;
         if constexpr (kW != 6) w4 = np[4];
-        if (has_tri && tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
+        if (has_tri && tri_test(sc, P0, P1, P2, f, s, L, wk) && anyhit) { done = true; return true; }
         if (do_node) {
             const uint32_t tb = thits | thits2;
             if constexpr (kW == 6) visit_words6(w0, w1, w2, w3);
@@ -652,10 +682,12 @@ struct Tracer8T {
             stats.tri();
             const uint32_t s = tbase + (uint32_t)__builtin_ctz(thits);
             thits &= thits - 1u;
-            const float4 t0 = sc.tris[(size_t)s * kTriQuads], t1 = sc.tris[(size_t)s * kTriQuads + 1], t2 = sc.tris[(size_t)s * kTriQuads + 2];
+            const float* f = tri_rec(sc, s) + rot();
+            V3 P0, P1, P2;
+            tri_vertices(f, P0, P1, P2);
             uint4 wk = make_uint4(0u, 0u, 0u, 0u);
             if constexpr (kLds) wk = *wrec(sc, L);
-            if (tri_test(sc, t0, t1, t2, s, L, wk) && anyhit) { done = true; return true; }
+            if (tri_test(sc, P0, P1, P2, f, s, L, wk) && anyhit) { done = true; return true; }
             return false;
         }
         if (!(nhits & 0xff000000u)) {
@@ -1465,8 +1497,10 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
     if (a.py) a.py[i] = a.oy[i] + t * a.dy[i];
     if (a.pz) a.pz[i] = a.oz[i] + t * a.dz[i];
     if (a.gnx || a.gny || a.gnz) {
-        const float4 p0 = a.sc.tris[(size_t)slot * kTriQuads], p1 = a.sc.tris[(size_t)slot * kTriQuads + 1],
-                     p2 = a.sc.tris[(size_t)slot * kTriQuads + 2];
+        V3 q0, q1, q2;
+        tri_vertices(tri_rec(a.sc, (uint32_t)slot), q0, q1, q2);
+        const float4 p0 = make_float4(q0.x, q0.y, q0.z, 0.0f), p1 = make_float4(q1.x, q1.y, q1.z, 0.0f),
+                     p2 = make_float4(q2.x, q2.y, q2.z, 0.0f);
         const V3 g = normalize(cross(v3(p1.x - p0.x, p1.y - p0.y, p1.z - p0.z),  // add_math.h:9-16
                                      v3(p2.x - p0.x, p2.y - p0.y, p2.z - p0.z)));
         if (a.gnx) a.gnx[i] = g.x;

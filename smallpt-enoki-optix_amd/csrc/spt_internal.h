@@ -10,10 +10,26 @@ namespace spt {
 
 constexpr uint32_t kMaxDepthCasts = 64;     // spt_render_params.max_depth limit
 constexpr uint32_t kNode8Quads = 8;         // BVH8 node stride in 16-B units (80 B used, padded to one 128-B line)
-#ifndef SPT_TRI_QUADS
-#define SPT_TRI_QUADS 3
-#endif
-constexpr uint32_t kTriQuads = SPT_TRI_QUADS;  // triangle record stride in 16-B units (3 used: v0 + id, v1, v2)
+// Triangle record: 16 floats, one 64-B half-line per BVH slot.  Each vertex is
+// stored as x y z x y (five floats), the original triangle id in float 15.  A
+// lane loads vertex i as the three floats at 5 i + r: r = 0 gives (x, y, z),
+// 1 gives (y, z, x), 2 gives (z, x, y) — the vertex already permuted into the
+// Woop test's (kx, ky, kz) order for a ray whose dominant axis is kz = (r + 2)
+// mod 3, so the test needs no per-lane component selects (spt_math.h
+// woop_shear_rot).
+constexpr uint32_t kTriQuads = 4;           // triangle record stride in 16-B units
+constexpr uint32_t kTriFloats = 16;
+constexpr uint32_t kTriIdFloat = 15;
+SPT_HD void tri_record_fill(float* rec, const float* v9, uint32_t id) {
+    for (int k = 0; k < 3; k++) {
+        rec[5 * k] = v9[3 * k];
+        rec[5 * k + 1] = v9[3 * k + 1];
+        rec[5 * k + 2] = v9[3 * k + 2];
+        rec[5 * k + 3] = v9[3 * k];
+        rec[5 * k + 4] = v9[3 * k + 1];
+    }
+    rec[kTriIdFloat] = u2f(id);
+}
 constexpr uint32_t kNode6Quads = 4;         // 64-B node (at most six children, bvh_build.h): one 64-B half-line
 constexpr uint32_t kIsectBlock = 128;       // isect: 2 waves, LDS stack [depth][128]
 #ifndef SPT_SHADE_BLOCK

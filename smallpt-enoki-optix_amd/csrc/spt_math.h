@@ -196,7 +196,13 @@ SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     int kx = kz + 1; if (kx == 3) kx = 0;
     int ky = kx + 1; if (ky == 3) ky = 0;
     float dkz = comp(d, kz);
-    if (dkz < 0.0f) { int tmp = kx; kx = ky; ky = tmp; }
+    // Woop et al. swap kx and ky when d_kz < 0 to keep the winding; this test
+    // accepts both windings, and with kx and ky swapped every edge function,
+    // det and T change sign exactly (IEEE round-to-nearest is symmetric), so
+    // t, u, v and every accept decision are bit-identical: the device keeps
+    // the cyclic order (kx, ky, kz), which the rotated triangle records hold
+    // (spt_internal.h); the oracle keeps the swap (oracle.c wray_setup), an
+    // independent check of that identity.
     WoopRay r;
     r.o = o; r.k = (uint32_t)kx | (uint32_t)ky << 2 | (uint32_t)kz << 4;
 #if SPT_WOOP_MULS
@@ -267,6 +273,21 @@ SPT_HD bool left_box_before_tmin(const WoopRay& r, const WoopShear& w, float Az,
     return (w.ey * asz) * kBoxPad < tmin * fabsf(r.Sy);
 }
 
+// The same shear from vertices and origin already in (kx, ky, kz) order
+// (rotated triangle records): A = P0 - O component by component, which is
+// comp(p0 - o, k) bit for bit.
+SPT_HD WoopShear woop_shear_rot(const WoopRay& r, V3 O, V3 P0, V3 P1, V3 P2) {
+    const V3 A = P0 - O, B = P1 - O, C = P2 - O;
+    WoopShear w;
+    w.Akz = A.z; w.Bkz = B.z; w.Ckz = C.z;
+    w.ex = exit_offset(A.x, B.x, C.x, r.Sx, r.Sz);
+    w.ey = exit_offset(A.y, B.y, C.y, r.Sy, r.Sz);
+    w.Ax = A.x - r.Sx * w.Akz; w.Ay = A.y - r.Sy * w.Akz;
+    w.Bx = B.x - r.Sx * w.Bkz; w.By = B.y - r.Sy * w.Bkz;
+    w.Cx = C.x - r.Sx * w.Ckz; w.Cy = C.y - r.Sy * w.Ckz;
+    return w;
+}
+
 struct NoReload {  // the vertices stay in registers (host)
     V3 p0, p1, p2;
     SPT_HD void operator()(V3& q0, V3& q1, V3& q2) const { q0 = p0; q1 = p1; q2 = p2; }
@@ -281,18 +302,15 @@ struct NoReload {  // the vertices stay in registers (host)
 // edge functions V, W with det, so a caller that keeps only the closest hit
 // divides once, u = V / det and v = W / det, for the hit it keeps (the same
 // correctly rounded quotients).
-template <typename Reload>
-SPT_HD bool woop_test_raw(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
-                          float& t_out, float& V_out, float& W_out, float& det_out) {
-    const WoopShear w = woop_shear(r, p0, p1, p2);
+template <typename Reshear>
+SPT_HD bool woop_core(const WoopRay& r, const WoopShear& w, Reshear reshear, float tmin, float tmax,
+                      float& t_out, float& V_out, float& W_out, float& det_out) {
     const float Akz = w.Akz, Bkz = w.Bkz, Ckz = w.Ckz;
     float U = w.Cx * w.By - w.Cy * w.Bx;
     float V = w.Ax * w.Cy - w.Ay * w.Cx;
     float W = w.Bx * w.Ay - w.By * w.Ax;
     if (U == 0.0f || V == 0.0f || W == 0.0f) {
-        V3 q0, q1, q2;
-        reload(q0, q1, q2);
-        const WoopShear x = woop_shear(r, q0, q1, q2);
+        const WoopShear x = reshear();
         // px qy - py qx for (p, q) = (C, B), (A, C), (B, A): one per iteration
         // of a rolled loop (the rotation keeps few doubles live at a time)
         float px = x.Cx, py = x.Cy, qx = x.Bx, qy = x.By, rx = x.Ax, ry = x.Ay;
@@ -323,11 +341,46 @@ SPT_HD bool woop_test_raw(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, 
     return true;
 }
 
+// The vertices in world order (the BVH2 tracer, the host).
+template <typename Reload>
+SPT_HD bool woop_test_raw(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
+                          float& t_out, float& V_out, float& W_out, float& det_out) {
+    const auto reshear = [&]() {
+        V3 q0, q1, q2;
+        reload(q0, q1, q2);
+        return woop_shear(r, q0, q1, q2);
+    };
+    return woop_core(r, woop_shear(r, p0, p1, p2), reshear, tmin, tmax, t_out, V_out, W_out, det_out);
+}
+
+// The vertices and origin already in (kx, ky, kz) order (rotated records):
+// reload() re-reads the rotated vertices.
+template <typename Reload>
+SPT_HD bool woop_test_raw_rot(const WoopRay& r, V3 O, V3 P0, V3 P1, V3 P2, Reload reload, float tmin, float tmax,
+                              float& t_out, float& V_out, float& W_out, float& det_out) {
+    const auto reshear = [&]() {
+        V3 q0, q1, q2;
+        reload(q0, q1, q2);
+        return woop_shear_rot(r, O, q0, q1, q2);
+    };
+    return woop_core(r, woop_shear_rot(r, O, P0, P1, P2), reshear, tmin, tmax, t_out, V_out, W_out, det_out);
+}
+
 template <typename Reload>
 SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, float tmin, float tmax,
                       float& t_out, float& u_out, float& v_out) {
     float V, W, det;
     if (!woop_test_raw(r, p0, p1, p2, reload, tmin, tmax, t_out, V, W, det)) return false;
+    u_out = V / det;
+    v_out = W / det;
+    return true;
+}
+
+template <typename Reload>
+SPT_HD bool woop_test_rot(const WoopRay& r, V3 O, V3 P0, V3 P1, V3 P2, Reload reload, float tmin, float tmax,
+                          float& t_out, float& u_out, float& v_out) {
+    float V, W, det;
+    if (!woop_test_raw_rot(r, O, P0, P1, P2, reload, tmin, tmax, t_out, V, W, det)) return false;
     u_out = V / det;
     v_out = W / det;
     return true;

@@ -17,7 +17,20 @@ from sptamd import _lib
 
 SECTIONS = ["nodes", "triangles", "normals", "texcoords", "orig2slot", "albedo", "emission", "spheres",
             "sphere materials", "material kinds", "texture sizes", "texels", "extra"]
-TRI_QUADS, NODE6_QUADS = 3, 4   # spt_internal.h kTriQuads / kNode6Quads
+TRI_QUADS, NODE6_QUADS = 4, 4   # spt_internal.h kTriQuads / kNode6Quads
+CACHE_VERSION = 2               # capi.cpp kCacheVersion (2: 64-B rotated triangle records)
+
+
+def tri_records(v9, ids):
+    """spt_internal.h tri_record_fill: per triangle 16 floats, each vertex as
+    x y z x y, the original id's bits in float 15."""
+    v = np.asarray(v9, np.float32).reshape(-1, 3, 3)
+    rec = np.zeros((v.shape[0], 16), np.float32)
+    for k in range(3):
+        rec[:, 5 * k:5 * k + 3] = v[:, k]
+        rec[:, 5 * k + 3:5 * k + 5] = v[:, k, :2]
+    rec[:, 15] = np.asarray(ids, np.uint32).view(np.float32)
+    return rec
 
 
 class Header(ctypes.Structure):
@@ -51,7 +64,7 @@ def sections():
     """A two-triangle six-wide scene with one 2 x 2 texture and extra bytes."""
     rng = np.random.default_rng(0)
     node = np.zeros(NODE6_QUADS * 4, np.uint32)
-    tris = rng.normal(size=(2 * TRI_QUADS, 4)).astype(np.float32)
+    tris = tri_records(rng.normal(size=(2, 9)), [1, 0])
     snrm = rng.normal(size=(2 * 3, 4)).astype(np.float32)
     return [node.tobytes(), tris.tobytes(), snrm.tobytes(), b"", np.array([1, 0], np.int32).tobytes(),
             np.full(3, 0.5, np.float32).tobytes(), b"", b"", b"", b"",
@@ -61,7 +74,7 @@ def sections():
 def header(secs, **over):
     h = Header()
     h.magic = b"SPTSCENE"
-    h.version, h.header_bytes = 1, ctypes.sizeof(Header)
+    h.version, h.header_bytes = CACHE_VERSION, ctypes.sizeof(Header)
     h.tri_quads, h.node_quads, h.node6, h.group_shift = TRI_QUADS, NODE6_QUADS, 1, 0
     h.config_bytes, h.stats_bytes = ctypes.sizeof(_lib.Config), ctypes.sizeof(_lib.SceneStats)
     h.stack_depth, h.nmat, h.nemit, h.nsph, h.nkind, h.ntexmat = 1, 1, 0, 0, 0, 1
@@ -133,7 +146,7 @@ def test_flipped_byte_refused(tmp_path, sec):
     assert "checksum" in msg and SECTIONS[sec] in msg
 
 
-@pytest.mark.parametrize("over", [dict(version=2), dict(tri_quads=4), dict(node_quads=8), dict(node6=0),
+@pytest.mark.parametrize("over", [dict(version=1), dict(tri_quads=3), dict(node_quads=8), dict(node6=0),
                                   dict(group_shift=1), dict(nmat=2), dict(ntri=3), dict(nsph=300),
                                   dict(stack_depth=0), dict(config_bytes=4)])
 def test_header_mismatch_refused(tmp_path, over):
