@@ -687,9 +687,11 @@ static inline int woop_test(const wray* r, const float* tv, float tmin, float tm
     if (fmaxf(fmaxf(Az, Bz), Cz) * BOX_PAD < tmin) return 0;
     if ((ex * fabsf(r->Sz)) * BOX_PAD < tmin * fabsf(r->Sx)) return 0;
     if ((ey * fabsf(r->Sz)) * BOX_PAD < tmin * fabsf(r->Sy)) return 0;
-    *t_out = t;
-    *u_out = V / det;
-    *v_out = W / det;
+    /* + 0.0f: a zero t, u or v is +0 (spt_math.h woop_core: its sign would
+     * follow det's, which the kx / ky order flips) */
+    *t_out = t + 0.0f;
+    *u_out = V / det + 0.0f;
+    *v_out = W / det + 0.0f;
     return 1;
 }
 

@@ -387,8 +387,8 @@ struct Tracer8T {
             x.id = tri_id(sc, r.x); x.u = u2f(r.z); x.v = u2f(r.w);
         } else {
             x.id = tri_id(sc, r.x);
-            x.u = u2f(r.y) / u2f(r.w);
-            x.v = u2f(r.z) / u2f(r.w);
+            x.u = u2f(r.y) / u2f(r.w) + 0.0f;  // as woop_test: a zero is +0
+            x.v = u2f(r.z) / u2f(r.w) + 0.0f;
         }
         return x;
     }

@@ -197,12 +197,13 @@ SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     int ky = kx + 1; if (ky == 3) ky = 0;
     float dkz = comp(d, kz);
     // Woop et al. swap kx and ky when d_kz < 0 to keep the winding; this test
-    // accepts both windings, and with kx and ky swapped every edge function,
-    // det and T change sign exactly (IEEE round-to-nearest is symmetric), so
-    // t, u, v and every accept decision are bit-identical: the device keeps
-    // the cyclic order (kx, ky, kz), which the rotated triangle records hold
-    // (spt_internal.h); the oracle keeps the swap (oracle.c wray_setup), an
-    // independent check of that identity.
+    // accepts both windings, and with kx and ky swapped every nonzero edge
+    // function, det and T change sign exactly (IEEE round-to-nearest is
+    // symmetric), so every accept decision and, with zeros made +0 (woop_core),
+    // every bit of t, u, v are the same: the device keeps the cyclic order
+    // (kx, ky, kz), which the rotated triangle records hold (spt_internal.h);
+    // the oracle keeps the swap (oracle.c wray_setup), an independent check of
+    // that identity (tests/test_woop_rotated.py).
     WoopRay r;
     r.o = o; r.k = (uint32_t)kx | (uint32_t)ky << 2 | (uint32_t)kz << 4;
 #if SPT_WOOP_MULS
@@ -334,7 +335,10 @@ SPT_HD bool woop_core(const WoopRay& r, const WoopShear& w, Reshear reshear, flo
 #if SPT_TRI_BOX_RULE
     if (left_box_before_tmin(r, w, Az, Bz, Cz, tmin)) return false;
 #endif
-    t_out = t;
+    // + 0.0f: a zero t, u or v is +0.  Its sign would otherwise follow det's,
+    // which the kx / ky order flips (the oracle keeps Woop's swap, the device
+    // does not): with it every output bit is independent of that order.
+    t_out = t + 0.0f;
     V_out = V;
     W_out = W;
     det_out = det;
@@ -371,8 +375,8 @@ SPT_HD bool woop_test(const WoopRay& r, V3 p0, V3 p1, V3 p2, Reload reload, floa
                       float& t_out, float& u_out, float& v_out) {
     float V, W, det;
     if (!woop_test_raw(r, p0, p1, p2, reload, tmin, tmax, t_out, V, W, det)) return false;
-    u_out = V / det;
-    v_out = W / det;
+    u_out = V / det + 0.0f;
+    v_out = W / det + 0.0f;
     return true;
 }
 
@@ -381,8 +385,8 @@ SPT_HD bool woop_test_rot(const WoopRay& r, V3 O, V3 P0, V3 P1, V3 P2, Reload re
                           float& t_out, float& u_out, float& v_out) {
     float V, W, det;
     if (!woop_test_raw_rot(r, O, P0, P1, P2, reload, tmin, tmax, t_out, V, W, det)) return false;
-    u_out = V / det;
-    v_out = W / det;
+    u_out = V / det + 0.0f;
+    v_out = W / det + 0.0f;
     return true;
 }
 

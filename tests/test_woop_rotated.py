@@ -1,0 +1,185 @@
+"""CPU check of the rotated triangle records (spt_internal.h tri_record_fill)
+and the Woop test without the kx / ky swap (spt_math.h woop_setup,
+woop_test_rot): the device's code path is compiled for the host with hipcc and
+run on random and adversarial triangle / ray pairs (axis-aligned, grazing,
+shared edges, origins on the plane, every dominant axis and sign), against a
+numpy restatement of the Woop-Benthin-Wald test WITH the swap (float32 op by
+op, the f64 edge fallback, oracle.c woop_test).  Claim under test: swapping kx
+and ky negates every edge function, det and T exactly, so (hit, t, u, v) are
+bit-identical — and a lane that loads its vertices rotated from the 64-B
+record (float 5 i + r) sees exactly the permuted components."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "smallpt-enoki-optix_amd", "csrc")
+
+MAIN = r"""
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "spt_internal.h"
+using namespace spt;
+struct RecReload {
+    const float* f;
+    void operator()(V3& a, V3& b, V3& c) const {
+        a = v3(f[0], f[1], f[2]); b = v3(f[5], f[6], f[7]); c = v3(f[10], f[11], f[12]);
+    }
+};
+int main(int argc, char** argv) {
+    FILE* in = fopen(argv[1], "rb");
+    FILE* out = fopen(argv[2], "wb");
+    int n = 0;
+    if (fread(&n, 4, 1, in) != 1) return 1;
+    std::vector<float> a((size_t)n * 17);
+    if (fread(a.data(), 4, a.size(), in) != a.size()) return 1;
+    for (int i = 0; i < n; i++) {
+        const float* x = &a[(size_t)i * 17];  // v0 v1 v2 (9), o (3), d (3), tmin, tmax
+        float rec[kTriFloats];
+        tri_record_fill(rec, x, 7u);
+        const V3 o = v3(x[9], x[10], x[11]), d = v3(x[12], x[13], x[14]);
+        const WoopRay wr = woop_setup(o, d);
+        const uint32_t kz = wr.k >> 4, r = kz == 2 ? 0 : kz + 1;
+        const float* f = rec + r;
+        const V3 O = r == 0 ? o : (r == 1 ? v3(o.y, o.z, o.x) : v3(o.z, o.x, o.y));
+        float t = 0, u = 0, v = 0;
+        const int hit = woop_test_rot(wr, O, v3(f[0], f[1], f[2]), v3(f[5], f[6], f[7]), v3(f[10], f[11], f[12]),
+                                      RecReload{f}, x[15], x[16], t, u, v) ? 1 : 0;
+        const float res[4] = {(float)hit, t, u, v};
+        fwrite(res, 4, 4, out);
+    }
+    fclose(out);
+    return 0;
+}
+"""
+
+
+@pytest.fixture(scope="module")
+def woop_host(tmp_path_factory):
+    hipcc = shutil.which("hipcc") or ("/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else None)
+    if not hipcc:
+        pytest.skip("hipcc not available")
+    d = tmp_path_factory.mktemp("woop")
+    cpp = d / "woop.cpp"
+    cpp.write_text(MAIN)
+    exe = d / "woop"
+    subprocess.run([hipcc, "-x", "hip", "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off", "-I", CSRC,
+                    "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(cpp)], check=True,
+                   capture_output=True)
+    return exe
+
+
+F = np.float32
+
+
+def woop_swapped(v, o, d, tmin, tmax):
+    """oracle.c woop_test (with the kx / ky swap and the box-exit rule), float32 op by op."""
+    ad = np.abs(d)
+    kz = (0 if ad[0] > ad[2] else 2) if ad[0] > ad[1] else (1 if ad[1] > ad[2] else 2)
+    kx = (kz + 1) % 3
+    ky = (kx + 1) % 3
+    if d[kz] < 0:
+        kx, ky = ky, kx
+    Sx, Sy, Sz = F(d[kx] / d[kz]), F(d[ky] / d[kz]), F(F(1) / d[kz])
+    A, B, C = (F(v[k] - o) for k in range(3))
+
+    def ex_(S, a, b, c):
+        neg = ((np.array(S, F).view(np.uint32) ^ np.array(Sz, F).view(np.uint32)) >> 31) != 0
+        return F(-min(min(a, b), c)) if neg else F(max(max(a, b), c))
+    ex = ex_(Sx, A[kx], B[kx], C[kx])
+    ey = ex_(Sy, A[ky], B[ky], C[ky])
+    Ax, Ay = F(A[kx] - F(Sx * A[kz])), F(A[ky] - F(Sy * A[kz]))
+    Bx, By = F(B[kx] - F(Sx * B[kz])), F(B[ky] - F(Sy * B[kz]))
+    Cx, Cy = F(C[kx] - F(Sx * C[kz])), F(C[ky] - F(Sy * C[kz]))
+    U = F(F(Cx * By) - F(Cy * Bx))
+    V = F(F(Ax * Cy) - F(Ay * Cx))
+    W = F(F(Bx * Ay) - F(By * Ax))
+    if U == 0 or V == 0 or W == 0:
+        dd = np.float64
+        U = F(dd(Cx) * dd(By) - dd(Cy) * dd(Bx))
+        V = F(dd(Ax) * dd(Cy) - dd(Ay) * dd(Cx))
+        W = F(dd(Bx) * dd(Ay) - dd(By) * dd(Ax))
+    if (U < 0 or V < 0 or W < 0) and (U > 0 or V > 0 or W > 0):
+        return 0, 0, 0, 0
+    det = F(F(U + V) + W)
+    if det == 0:
+        return 0, 0, 0, 0
+    Az, Bz, Cz = F(Sz * A[kz]), F(Sz * B[kz]), F(Sz * C[kz])
+    T = F(F(F(U * Az) + F(V * Bz)) + F(W * Cz))
+    t = F(T / det)
+    if not (t >= tmin and t <= tmax):
+        return 0, 0, 0, 0
+    pad = F(1.000001)
+    if F(F(max(max(Az, Bz), Cz)) * pad) < tmin:
+        return 0, 0, 0, 0
+    if F(F(ex * abs(Sz)) * pad) < F(tmin * abs(Sx)) or F(F(ey * abs(Sz)) * pad) < F(tmin * abs(Sy)):
+        return 0, 0, 0, 0
+    return 1, F(t + F(0)), F(F(V / det) + F(0)), F(F(W / det) + F(0))
+
+
+def cases(n, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        kind = i % 6
+        if kind == 0:    # random triangle, ray toward its interior
+            v = rng.normal(size=(3, 3)).astype(F)
+            tgt = (v * rng.dirichlet([1, 1, 1])[:, None]).sum(0)
+            o = rng.normal(size=3).astype(F) * F(3)
+        elif kind == 1:  # axis-aligned triangle, ray along a random dominant axis
+            ax = rng.integers(3)
+            v = rng.uniform(-1, 1, size=(3, 3)).astype(F)
+            v[:, ax] = F(rng.uniform(-1, 1))
+            tgt = (v * rng.dirichlet([1, 1, 1])[:, None]).sum(0)
+            o = tgt.copy()
+            o[ax] += F(rng.choice([-1, 1]) * rng.uniform(0.0005, 3))
+        elif kind == 2:  # ray through a shared edge / vertex
+            v = rng.normal(size=(3, 3)).astype(F)
+            w = rng.uniform(0, 1)
+            tgt = (v[0] * w + v[1] * (1 - w)) if rng.random() < 0.7 else v[2]
+            o = rng.normal(size=3).astype(F) * F(2)
+        elif kind == 3:  # grazing: origin near the plane
+            v = rng.normal(size=(3, 3)).astype(F)
+            nrm = np.cross(v[1] - v[0], v[2] - v[0])
+            nrm /= np.linalg.norm(nrm)
+            tgt = (v * rng.dirichlet([1, 1, 1])[:, None]).sum(0)
+            o = (tgt + rng.normal(size=3) * 0.5 + nrm * rng.uniform(-1e-3, 1e-3)).astype(F)
+        elif kind == 4:  # origin on the triangle's plane (a leaving ray), near tmin
+            v = rng.normal(size=(3, 3)).astype(F)
+            o = (v * rng.dirichlet([1, 1, 1])[:, None]).sum(0).astype(F)
+            tgt = o + rng.normal(size=3) * 0.01
+        else:            # huge / tiny scales
+            s = F(10.0 ** rng.uniform(-3, 3))
+            v = (rng.normal(size=(3, 3)) * s).astype(F)
+            tgt = (v * rng.dirichlet([1, 1, 1])[:, None]).sum(0)
+            o = (rng.normal(size=3) * s * 3).astype(F)
+        d = (np.asarray(tgt, np.float64) - o).astype(F)
+        if rng.random() < 0.5:
+            d = -d if rng.random() < 0.2 else d
+        tmin = F(0.001) if rng.random() < 0.8 else F(0)
+        out.append(np.concatenate([v.reshape(9), o, d, [tmin, F(1e20)]]).astype(F))
+    return np.stack(out)
+
+
+def test_rotated_records_and_unswapped_woop_bitexact(woop_host, tmp_path):
+    x = cases(20000, seed=5)
+    fin = tmp_path / "in.bin"
+    with open(fin, "wb") as f:
+        f.write(np.int32(len(x)).tobytes())
+        f.write(x.tobytes())
+    fout = tmp_path / "out.bin"
+    subprocess.run([str(woop_host), str(fin), str(fout)], check=True, timeout=60)
+    got = np.fromfile(fout, F).reshape(-1, 4)
+    hits = 0
+    for i, row in enumerate(x):
+        want = woop_swapped(row[:9].reshape(3, 3), row[9:12], row[12:15], row[15], row[16])
+        g = (int(got[i, 0]), got[i, 1], got[i, 2], got[i, 3])
+        assert g[0] == want[0], (i, g, want)
+        if want[0]:
+            hits += 1
+            assert np.array([g[1], g[2], g[3]], F).tobytes() == np.array(want[1:], F).tobytes(), (i, g, want)
+    assert hits > 5000
