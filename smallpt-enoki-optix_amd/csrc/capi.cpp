@@ -86,7 +86,16 @@ struct Counters {
     alignas(128) uint32_t isect_next; // persistent isect work counter (zeroed by each refill)
     uint32_t exhausted;  // RefillArgs::iter_tag of the refill that started the last work item (0: not yet)
     uint32_t pad[2];
+    alignas(128) uint32_t isect_next_b;  // SPT_ISECT_CAMERA: the counter of the launches on queue 1
 };
+uint32_t* isect_next_of(Counters* c, int queue) { return queue ? &c->isect_next_b : &c->isect_next; }
+
+// Camera paths started inside the isect launches (no refill launch per
+// iteration): an experiment, VERDICT r3 item 3 (EXPERIMENTS.md round 4).
+#ifndef SPT_ISECT_CAMERA
+#define SPT_ISECT_CAMERA 0
+#endif
+constexpr bool kIsectCam = SPT_ISECT_CAMERA != 0;
 
 // Render-wide device statistics.
 struct Stats {
@@ -1932,7 +1941,9 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             sub_begin[k] = wb;
             sub_end[k] = we;
             started[k] = wb + first;
-            if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], first, strm[k]); }))) return st;
+            // (SPT_ISECT_CAMERA: the first isect launch starts these paths)
+            if (!kIsectCam && (st = mark(0, strm[k], [&] { return launch_refill(ra[k], first, strm[k]); })))
+                return st;
         }
         // isect -> shade -> refill per sub-wavefront until every queue drains.
         // A path cast in iteration i was started by the refill after iteration
@@ -1975,9 +1986,28 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                     const int c = cur[k], nx = 1 - c;
                     ia[k].q = q[k][c];
                     ia[k].count = &b.cnt->qn[c];
+                    const bool cam = kIsectCam && !trav_stats;
+                    if (cam) {
+                        // survivors in q[c] (surv[c]) plus new camera paths after
+                        // them; the previous launch (queue nx) left its cursor in
+                        // cursor[nx]; this one's shade appends to surv[nx]
+                        RefillArgs& R = ia[k].cam;
+                        R = ra[k];
+                        R.q = q[k][c];
+                        R.surv = &b.cnt->surv[c];
+                        R.cursor_in = it == 0 ? nullptr : &b.cnt->cursor[nx];
+                        R.cursor_out = &b.cnt->cursor[c];
+                        R.qn_out = &b.cnt->qn[c];
+                        R.isect_next = isect_next_of(b.cnt, nx);
+                        R.surv_clear = &b.cnt->surv[nx];
+                        R.casts_in = nullptr;
+                        R.iter_tag = (uint32_t)it + 1;
+                        ia[k].next = isect_next_of(b.cnt, c);
+                    }
                     if ((st = mark(1, strm[k], [&] {
                              return trav_stats ? launch_isect_queue_stats(ia[k], known[k], strm[k])
-                                               : launch_isect_queue(ia[k], known[k], strm[k]);
+                                               : cam ? launch_isect_queue_cam(ia[k], known[k], strm[k])
+                                                     : launch_isect_queue(ia[k], known[k], strm[k]);
                          })))
                         return st;
                     // surv[nx] was zeroed by the previous refill (surv_clear)
@@ -1985,6 +2015,10 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                     sa[k].count_in = &b.cnt->qn[c];
                     sa[k].count_out = &b.cnt->surv[nx];
                     if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], mode, known[k], strm[k]); }))) return st;
+                    if (cam) {  // no refill launch: the next isect starts the new paths
+                        cur[k] = nx;
+                        continue;
+                    }
                     ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
                     ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
                     ra[k].surv_clear = &b.cnt->surv[c];
@@ -2013,8 +2047,19 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                 if (pending[k] >= 0) {
                     HIP_TRY(hipEventSynchronize(b.count_ev[pending[k]]));
                     const Counters& hc = b.host_cnt[pending[k]];
-                    known[k] = hc.qn[pend_cur[k]];
-                    started[k] = std::max<uint64_t>(started[k], hc.cursor[pend_cur[k]]);
+                    if (kIsectCam && !trav_stats) {
+                        // after an isect on queue 1 - pend_cur and its shade into
+                        // pend_cur: the next launch holds those survivors plus as
+                        // many new paths as fit
+                        const uint32_t sv = hc.surv[pend_cur[k]];
+                        const uint64_t cu = hc.cursor[1 - pend_cur[k]];
+                        started[k] = std::max<uint64_t>(started[k], cu);
+                        const uint64_t left = sub_end[k] > started[k] ? sub_end[k] - started[k] : 0;
+                        known[k] = (uint32_t)std::min<uint64_t>(ws.sub[k].cap, sv + left);
+                    } else {
+                        known[k] = hc.qn[pend_cur[k]];
+                        started[k] = std::max<uint64_t>(started[k], hc.cursor[pend_cur[k]]);
+                    }
                     if (known[k] == 0) {
                         live[k] = false;
                         nlive--;

@@ -740,12 +740,57 @@ __device__ __forceinline__ TraceHit trace(const DeviceScene& sc, V3 o, V3 d, flo
 // quarter from the launch-wide counter *a.next, which evens out the tail.
 // The last cast of a path only needs a yes/no answer (a miss is the only thing
 // that contributes, main.cpp:407), so it runs as an any-hit query.
-template <typename Tr, bool kStats>
-__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(kStats ? 1 : Tr::kMinWaves, 8)))
+__device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32_t order, uint32_t x, uint32_t y,
+                                           V3& o, V3& d);
+
+// A new camera path for work item w (refill_kernel's arithmetic): its ray,
+// tile pixel p and meta (sample << 8, cast 0).
+__device__ __forceinline__ void start_path(const RefillArgs& r, uint64_t w, V3& o, V3& d, uint32_t& p, uint32_t& meta) {
+    uint32_t s, q, lx, ly;
+    work_item((uint32_t)(w - (uint64_t)r.chunk_s0 * r.P), r.chunk_s0, r.chunk_ns, r.P, r.work_order != 0, s, q);
+    work_pixel(q, r.W, r.P, r.pixel_block, lx, ly);
+    p = ly * r.W + lx;
+    const uint32_t gy = tile_global_row(ly, r.tile_index, r.tile_count, r.rows_per_group);
+    const uint32_t gpix = gy * r.W + lx;                    // main.cpp:379-382
+    Pcg32 rng;
+    rng.seed(r.initstate, (uint64_t)gpix);                   // main.cpp:376
+    rng.state = pcg_apply(r.sample_jump[s], rng.state, rng.inc);
+    camera_ray(r.cam, rng, r.rng_order, lx, gy, o, d);
+    meta = s << kMetaDepthBits;
+}
+
+#ifndef SPT_ISECT_CAM_WAVES
+#define SPT_ISECT_CAM_WAVES 8
+#endif
+template <typename Tr, bool kStats, bool kCam = false>
+__global__ __launch_bounds__(kIsectBlock)
+__attribute__((amdgpu_waves_per_eu(kStats ? 1 : (kCam ? SPT_ISECT_CAM_WAVES : Tr::kMinWaves), 8)))
 void isect_queue_kernel(IsectQueueArgs a) {
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
-    const uint32_t n = *a.count;
+    uint32_t n, nq = 0;
+    uint64_t cur = 0;
+    if constexpr (kCam) {
+        // survivors in [0, nq), new camera paths in [nq, n) (refill_kernel's rule)
+        nq = wave_uniform(*a.cam.surv);
+        cur = a.cam.cursor_in ? *a.cam.cursor_in : a.cam.cursor_init;
+        const uint64_t avail = a.cam.work_end > cur ? a.cam.work_end - cur : 0;
+        const uint32_t room = a.cam.capacity - nq;
+        const uint32_t total = (uint32_t)(avail < room ? avail : room);
+        n = nq + total;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            *a.cam.cursor_out = cur + total;
+            *a.cam.qn_out = n;
+            *a.cam.isect_next = 0;  // the next launch's work counter
+            *a.cam.surv_clear = 0;  // the shade after this launch appends survivors there
+            if (cur < a.cam.work_end && cur + total >= a.cam.work_end) *a.cam.exhausted = a.cam.iter_tag;
+            if (n) atomicAdd(&a.cam.stats[0], (unsigned long long)n);       // casts
+            if (nq) atomicAdd(&a.cam.stats[1], (unsigned long long)nq);     // continuations
+            if (total) atomicAdd(&a.cam.stats[2], (unsigned long long)total);  // camera paths started
+        }
+    } else {
+        n = *a.count;
+    }
     typename std::conditional<kStats, TravStats, NoStats>::type st;
     Tr tr;
     uint32_t ray = 0;
@@ -777,10 +822,23 @@ void isect_queue_kernel(IsectQueueArgs a) {
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
                 if (!busy && rank < take) {
                     ray = pool + rank;
-                    const float4 q1 = ldq(a.q.q1 + ray), q2 = ldq(a.q.q2 + ray);
-                    const V3 o = v3(q1.x, q1.y, q1.z);
-                    const V3 d = v3(q2.x, q2.y, q2.z);
-                    const uint32_t depth = f2u(q1.w) & ((1u << kMetaDepthBits) - 1u);
+                    V3 o, d;
+                    uint32_t depth;
+                    if (!kCam || ray < nq) {
+                        const float4 q1 = ldq(a.q.q1 + ray), q2 = ldq(a.q.q2 + ray);
+                        o = v3(q1.x, q1.y, q1.z);
+                        d = v3(q2.x, q2.y, q2.z);
+                        depth = f2u(q1.w) & ((1u << kMetaDepthBits) - 1u);
+                    } else {
+                        // a new camera path: its ray is made here and stored for the shade
+                        uint32_t p, meta;
+                        start_path(a.cam, cur + (ray - nq), o, d, p, meta);
+                        stq(a.q.q1 + ray, make_float4(o.x, o.y, o.z, u2f(meta)));
+                        stq(a.q.q2 + ray, make_float4(d.x, d.y, d.z, u2f(p)));
+                        if (a.cam.mode >= kModeAlbedo) stq(a.q.q0 + ray, make_float4(1.0f, 1.0f, 1.0f, 0.0f));
+                        if (a.cam.mode == kModeEmit) stq2(a.q.rad + ray, make_float2(0.0f, 0.0f));
+                        depth = 0;
+                    }
                     // any-hit for the last cast unless emitters need the surface
                     tr.init(a.sc, o, d, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !a.sc.emission, L);
                     busy = !tr.finished();
@@ -917,8 +975,8 @@ void isect_public_persistent_kernel(IsectPublicArgs a) {
 }
 
 // ------------------------------------------------------------ camera gen
-__device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32_t order, uint32_t x,
-                                           uint32_t y, V3& o, V3& d) {
+__device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32_t order, uint32_t x, uint32_t y,
+                                           V3& o, V3& d) {
     float xi_x, xi_y;
     draw2(rng, order, xi_x, xi_y);              // main.cpp:395
     o = camera_sample_pos(cam, xi_x, xi_y);
@@ -1532,7 +1590,7 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
 static inline uint32_t blocks_for(uint32_t items, uint32_t block) { return (items + block - 1) / block; }
 
 // Workgroups resident on the whole chip for this LDS stack size (cached).
-template <typename Tr, bool kStats>
+template <typename Tr, bool kStats, bool kCam>
 static uint32_t persistent_blocks(size_t lds) {
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
@@ -1541,7 +1599,7 @@ static uint32_t persistent_blocks(size_t lds) {
     (void)hipGetDevice(&dev);
     if (cached && cached_lds == lds && cached_dev == dev) return cached;
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<Tr, kStats>, kIsectBlock, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<Tr, kStats, kCam>, kIsectBlock, lds) !=
             hipSuccess || per_cu <= 0)
         per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
@@ -1551,14 +1609,14 @@ static uint32_t persistent_blocks(size_t lds) {
     return cached;
 }
 
-template <typename Tr, bool kStats>
+template <typename Tr, bool kStats, bool kCam = false>
 static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
     const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
-    const uint32_t full = persistent_blocks<Tr, kStats>(lds);
+    const uint32_t full = persistent_blocks<Tr, kStats, kCam>(lds);
     const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)full * a.grid_q8) >> 8)) : full;
     const uint32_t blocks = min(scaled, blocks_for(grid_items, kIsectBlock));
-    hipLaunchKernelGGL((isect_queue_kernel<Tr, kStats>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
+    hipLaunchKernelGGL((isect_queue_kernel<Tr, kStats, kCam>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1566,6 +1624,13 @@ hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipS
     if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false>(a, grid_items, s);
     return a.sc.node6 ? launch_isect_queue_t<Tracer6, false>(a, grid_items, s)
                       : launch_isect_queue_t<Tracer8, false>(a, grid_items, s);
+}
+
+// the isect launch that also starts the camera paths (IsectQueueArgs::cam)
+hipError_t launch_isect_queue_cam(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+    if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false, true>(a, grid_items, s);
+    return a.sc.node6 ? launch_isect_queue_t<Tracer6, false, true>(a, grid_items, s)
+                      : launch_isect_queue_t<Tracer8, false, true>(a, grid_items, s);
 }
 
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {

@@ -224,6 +224,32 @@ SPT_HD V3 reflectance(const DeviceScene& sc, uint32_t mat, uint32_t slot, float 
     return v3(sc.albedo[mat * 3], sc.albedo[mat * 3 + 1], sc.albedo[mat * 3 + 2]);
 }
 
+struct RefillArgs {
+    PathQueue q;
+    Camera cam;
+    const uint32_t* surv;       // survivors already in the queue
+    const uint64_t* cursor_in;  // null: start at cursor_init (the first refill of a chunk)
+    uint64_t cursor_init;
+    uint64_t* cursor_out;       // written by thread 0 only
+    uint32_t* qn_out;           // queue count for the next isect, thread 0 only
+    uint32_t* isect_next;       // zeroed by thread 0 for the next isect launch
+    uint32_t* surv_clear;       // zeroed by thread 0: the next shade's survivor counter (may be null)
+    const uint32_t* casts_in;   // the preceding shade's queue count (null for a chunk's first refill):
+                                // thread 0 adds it and *surv to stats[0] / stats[1]
+    const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
+    unsigned long long* stats;  // casts, continuations, regenerations
+    uint32_t* exhausted;        // thread 0 writes iter_tag here when this refill starts the last work item
+    uint32_t iter_tag;          // the host's iteration number + 2 (the chunk's first refill: 1)
+    uint64_t work_end;          // W_total (work items of this chunk end here)
+    uint32_t capacity, P, W, rng_order;
+    uint32_t tile_index, tile_count, rows_per_group;
+    uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
+    uint32_t work_order;        // 0: sample-major work items, 1: pixel-major inside the chunk
+    uint32_t chunk_s0, chunk_ns;  // the chunk's first sample and sample count
+    uint64_t initstate;
+    int mode;                   // PathMode: which planes a new path fills
+};
+
 struct IsectQueueArgs {
     DeviceScene sc;
     PathQueue q;
@@ -237,6 +263,12 @@ struct IsectQueueArgs {
     uint32_t grid_q8;                // persistent grid scale in 1/256ths of full occupancy (0 = full)
     uint32_t xcd_remap;              // 1: blocks sharing an XCD take adjacent static shares
     unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
+    // Camera paths started inside the launch (SPT_ISECT_CAMERA): the queue
+    // holds cam.surv survivors in slots [0, surv); the launch starts
+    // min(capacity - surv, work left) new camera paths in the slots after them
+    // (writing their rays for the shade) and does refill_kernel's bookkeeping
+    // in block 0's first thread (cam.isect_next: the NEXT launch's counter).
+    RefillArgs cam;
 };
 
 struct IsectPublicArgs {
@@ -282,31 +314,6 @@ struct ShadeArgs {
 
 // Starts new paths in queue slots [*surv, capacity): work item w (sample-major:
 // sample = w / P, tile pixel = w % P) for w in [*cursor_in, W_total).
-struct RefillArgs {
-    PathQueue q;
-    Camera cam;
-    const uint32_t* surv;       // survivors already in the queue
-    const uint64_t* cursor_in;  // null: start at cursor_init (the first refill of a chunk)
-    uint64_t cursor_init;
-    uint64_t* cursor_out;       // written by thread 0 only
-    uint32_t* qn_out;           // queue count for the next isect, thread 0 only
-    uint32_t* isect_next;       // zeroed by thread 0 for the next isect launch
-    uint32_t* surv_clear;       // zeroed by thread 0: the next shade's survivor counter (may be null)
-    const uint32_t* casts_in;   // the preceding shade's queue count (null for a chunk's first refill):
-                                // thread 0 adds it and *surv to stats[0] / stats[1]
-    const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
-    unsigned long long* stats;  // casts, continuations, regenerations
-    uint32_t* exhausted;        // thread 0 writes iter_tag here when this refill starts the last work item
-    uint32_t iter_tag;          // the host's iteration number + 2 (the chunk's first refill: 1)
-    uint64_t work_end;          // W_total (work items of this chunk end here)
-    uint32_t capacity, P, W, rng_order;
-    uint32_t tile_index, tile_count, rows_per_group;
-    uint32_t pixel_block;       // camera-path order: B x B pixel blocks (<= 1: scanline)
-    uint32_t work_order;        // 0: sample-major work items, 1: pixel-major inside the chunk
-    uint32_t chunk_s0, chunk_ns;  // the chunk's first sample and sample count
-    uint64_t initstate;
-    int mode;                   // PathMode: which planes a new path fills
-};
 
 // Fused persistent render (one launch per sample chunk): every lane owns a
 // path from camera ray to termination — trace, shade, bounce in registers.
@@ -397,6 +404,7 @@ SPT_HD void work_pixel(uint32_t q, uint32_t W, uint32_t P, uint32_t B, uint32_t&
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
+hipError_t launch_isect_queue_cam(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
 hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out);
 hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s);
