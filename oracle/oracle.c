@@ -608,9 +608,10 @@ static inline void wray_setup(wray* r) {
     int ky = kx + 1; if (ky == 3) ky = 0;
     if (r->d[kz] < 0.0f) { int tmp = kx; kx = ky; ky = tmp; }
     r->kx = kx; r->ky = ky; r->kz = kz;
-    r->Sx = r->d[kx] / r->d[kz];
-    r->Sy = r->d[ky] / r->d[kz];
+    /* one divide, two products (spt_math.h woop_setup) */
     r->Sz = 1.0f / r->d[kz];
+    r->Sx = r->d[kx] * r->Sz;
+    r->Sy = r->d[ky] * r->Sz;
     for (int k = 0; k < 3; k++) r->inv[k] = 1.0f / r->d[k];
 }
 

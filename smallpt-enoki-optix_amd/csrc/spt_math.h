@@ -187,9 +187,6 @@ struct WoopRay {
     SPT_HD int ky() const { return (int)((k >> 2) & 3u); }
     SPT_HD int kz() const { return (int)(k >> 4); }
 };
-#ifndef SPT_WOOP_MULS
-#define SPT_WOOP_MULS 0
-#endif
 SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
     int kz = (ax > ay) ? ((ax > az) ? 0 : 2) : ((ay > az) ? 1 : 2);
@@ -206,15 +203,12 @@ SPT_HD WoopRay woop_setup(V3 o, V3 d) {
     // that identity (tests/test_woop_rotated.py).
     WoopRay r;
     r.o = o; r.k = (uint32_t)kx | (uint32_t)ky << 2 | (uint32_t)kz << 4;
-#if SPT_WOOP_MULS
+    // one correctly rounded divide, then two products (Woop et al. divide
+    // three times): config 1 +1.1 % from the ray set-up alone; the oracle
+    // computes the same (oracle.c wray_setup)
     r.Sz = 1.0f / dkz;
     r.Sx = comp(d, kx) * r.Sz;
     r.Sy = comp(d, ky) * r.Sz;
-#else
-    r.Sx = comp(d, kx) / dkz;
-    r.Sy = comp(d, ky) / dkz;
-    r.Sz = 1.0f / dkz;
-#endif
     return r;
 }
 

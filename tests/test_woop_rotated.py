@@ -84,7 +84,8 @@ def woop_swapped(v, o, d, tmin, tmax):
     ky = (kx + 1) % 3
     if d[kz] < 0:
         kx, ky = ky, kx
-    Sx, Sy, Sz = F(d[kx] / d[kz]), F(d[ky] / d[kz]), F(F(1) / d[kz])
+    Sz = F(F(1) / d[kz])
+    Sx, Sy = F(d[kx] * Sz), F(d[ky] * Sz)
     A, B, C = (F(v[k] - o) for k in range(3))
 
     def ex_(S, a, b, c):

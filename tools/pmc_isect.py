@@ -65,6 +65,9 @@ def main(out, key, log, *paths):
            # the library build the passes measured (spt_build_id): bench.py uses
            # this entry only while the loaded libspt.so reports the same id
            "build_id": roof.get("build_id"),
+           # hardware queues the profiled process ran with (bench.py requests 8;
+           # under rocprofv3 the runtime may start first, so both are recorded)
+           "hw_queues": b["config"].get("hw_queues"),
            f"{unit}s_per_launch": casts, "dispatches": {c: len(v) for c, v in per.items()}, "per_launch": mean,
            "source": [os.path.relpath(p) for p in paths]}
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
