@@ -203,6 +203,7 @@ struct Workspace {
     size_t jump_cap = 0;
     PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps (read-only)
     uint32_t jump_key_spp = 0, jump_key_depth = 0;
+    uint64_t jump_key_state = 0;
     RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
     uint64_t next_ticket = 1;
     hipEvent_t epoch = nullptr;         // the first timed render's time origin: isect_begin/end_ms count from it
@@ -380,8 +381,12 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
 // each sample's first draw, s * (4 + 2D), and from there to the bounce draw
 // of each cast, 4 + 2 * cast (main.cpp:395,396,413).  Rewritten only when
 // spp or depth change, after every queued render has finished with it.
-spt_status ensure_jumps(Workspace& w, uint32_t spp, uint32_t depth) {
-    if (w.jumps && w.jump_key_spp == spp && w.jump_key_depth == depth) return SPT_OK;
+// [spp] per sample: seed(initstate, .) then the jump past s * (4 + 2D) draws,
+// as one affine map of the stream constant (spt_math.h pcg_seeded_jump);
+// then [depth] per cast: the jump past 4 + 2 cast draws.
+spt_status ensure_jumps(Workspace& w, uint32_t spp, uint32_t depth, uint64_t initstate) {
+    if (w.jumps && w.jump_key_spp == spp && w.jump_key_depth == depth && w.jump_key_state == initstate)
+        return SPT_OK;
     if (w.jumps) HIP_TRY(hipDeviceSynchronize());
     const size_t n = (size_t)spp + kMaxDepthCasts;
     if (n > w.jump_cap) {
@@ -392,11 +397,12 @@ spt_status ensure_jumps(Workspace& w, uint32_t spp, uint32_t depth) {
     }
     const uint64_t per_sample = 4ull + 2ull * depth;
     std::vector<PcgJump> jt((size_t)spp + depth);
-    for (uint32_t s = 0; s < spp; s++) jt[s] = pcg_jump_coeffs((uint64_t)s * per_sample);
+    for (uint32_t s = 0; s < spp; s++) jt[s] = pcg_seeded_jump(initstate, pcg_jump_coeffs((uint64_t)s * per_sample));
     for (uint32_t j = 0; j < depth; j++) jt[(size_t)spp + j] = pcg_jump_coeffs(4ull + 2ull * j);
     HIP_TRY(hipMemcpy(w.jumps, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
     w.jump_key_spp = spp;
     w.jump_key_depth = depth;
+    w.jump_key_state = initstate;
     return SPT_OK;
 }
 
@@ -1736,7 +1742,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     ws.last_ticket = sc->ws.next_ticket;
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P);
     if (st) return st;
-    if ((st = ensure_jumps(sc->ws, p.spp, p.max_depth))) return st;
+    if ((st = ensure_jumps(sc->ws, p.spp, p.max_depth, p.rng_initstate))) return st;
     const PcgJump* jumps = sc->ws.jumps;
     // HIP events around the isect launches (the roofline kernel); every other
     // launch only with SPT_FLAG_TIMING_ALL (each event pair costs host time).

@@ -309,6 +309,8 @@ struct Tracer {
 // each axis is widened by a margin that bounds the fp32 error of that form
 // relative to the exact quantised planes (which already enclose the child),
 // so culling stays conservative and the closest hit is the exact Woop one.
+// (the margin is formed as one mul and one fma: it bounds the rounding of the
+// slab form with several ulps to spare, so its own rounding does not matter)
 constexpr float kMarginRel = 1e-6f;
 // Step modes (template argument of Tracer8T): 0 = one triangle test OR one
 // node visit per step; 1 = the last triangle of a group rides along with the
@@ -473,9 +475,9 @@ struct Tracer8T {
         const float bx = (u2f(q0.x) - o.x) * ix;
         const float by = (u2f(q0.y) - o.y) * iy;
         const float bz = (u2f(q0.z) - o.z) * iz;
-        const float mx = (fabsf(bx) + 255.0f * fabsf(ax)) * kMarginRel;
-        const float my = (fabsf(by) + 255.0f * fabsf(ay)) * kMarginRel;
-        const float mz = (fabsf(bz) + 255.0f * fabsf(az)) * kMarginRel;
+        const float mx = fmaf(fabsf(ax), 255.0f * kMarginRel, fabsf(bx) * kMarginRel);
+        const float my = fmaf(fabsf(ay), 255.0f * kMarginRel, fabsf(by) * kMarginRel);
+        const float mz = fmaf(fabsf(az), 255.0f * kMarginRel, fabsf(bz) * kMarginRel);
         const float bxe = bx - mx, bxx = bx + mx, bye = by - my, byx = by + my, bze = bz - mz, bzx = bz + mz;
         const bool px = ix >= 0.0f, py = iy >= 0.0f, pz = iz >= 0.0f;
         const uint32_t exl = px ? q1.w : q2.x, xxl = px ? q2.x : q1.w;
@@ -515,9 +517,9 @@ struct Tracer8T {
         const float bx = (u2f(w0.x) - o.x) * ix;
         const float by = (u2f(w0.y) - o.y) * iy;
         const float bz = (u2f(w0.z) - o.z) * iz;
-        const float mx = (fabsf(bx) + 255.0f * fabsf(ax)) * kMarginRel;
-        const float my = (fabsf(by) + 255.0f * fabsf(ay)) * kMarginRel;
-        const float mz = (fabsf(bz) + 255.0f * fabsf(az)) * kMarginRel;
+        const float mx = fmaf(fabsf(ax), 255.0f * kMarginRel, fabsf(bx) * kMarginRel);
+        const float my = fmaf(fabsf(ay), 255.0f * kMarginRel, fabsf(by) * kMarginRel);
+        const float mz = fmaf(fabsf(az), 255.0f * kMarginRel, fabsf(bz) * kMarginRel);
         const float bxe = bx - mx, bxx = bx + mx, bye = by - my, byx = by + my, bze = bz - mz, bzx = bz + mz;
         // entry planes are the lo planes for a positive direction, hi otherwise
         const bool px = ix >= 0.0f, py = iy >= 0.0f, pz = iz >= 0.0f;
@@ -752,9 +754,7 @@ __device__ __forceinline__ void start_path(const RefillArgs& r, uint64_t w, V3& 
     p = ly * r.W + lx;
     const uint32_t gy = tile_global_row(ly, r.tile_index, r.tile_count, r.rows_per_group);
     const uint32_t gpix = gy * r.W + lx;                    // main.cpp:379-382
-    Pcg32 rng;
-    rng.seed(r.initstate, (uint64_t)gpix);                   // main.cpp:376
-    rng.state = pcg_apply(r.sample_jump[s], rng.state, rng.inc);
+    Pcg32 rng = pcg_start(r.sample_jump[s], (uint64_t)gpix);  // main.cpp:376, then the sample's draws
     camera_ray(r.cam, rng, r.rng_order, lx, gy, o, d);
     meta = s << kMetaDepthBits;
 }
@@ -997,10 +997,9 @@ __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o,
 // PCG32 of global pixel gpix (main.cpp:376) advanced past the draws a path
 // has consumed: the sample's jump (s * (4 + 2D)) then the cast's (4 camera
 // draws + 2 per earlier cast, main.cpp:395,396,413).
-__device__ __forceinline__ Pcg32 path_rng(uint64_t initstate, uint32_t gpix, const PcgJump& js, const PcgJump& jc) {
-    Pcg32 r;
-    r.seed(initstate, (uint64_t)gpix);
-    r.state = pcg_apply(js, r.state, r.inc);
+// (js: the seeded sample map of pcg_seeded_jump, capi.cpp ensure_jumps)
+__device__ __forceinline__ Pcg32 path_rng(uint32_t gpix, const PcgJump& js, const PcgJump& jc) {
+    Pcg32 r = pcg_start(js, (uint64_t)gpix);
     r.state = pcg_apply(jc, r.state, r.inc);
     return r;
 }
@@ -1056,9 +1055,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         const uint32_t p = ly * a.W + lx;
         const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
         const uint32_t gpix = gy * a.W + lx;                    // main.cpp:379-382
-        Pcg32 rng;
-        rng.seed(a.initstate, (uint64_t)gpix);                   // main.cpp:376
-        rng.state = pcg_apply(a.sample_jump[s], rng.state, rng.inc);
+        Pcg32 rng = pcg_start(a.sample_jump[s], (uint64_t)gpix);  // main.cpp:376, then the sample's draws
         V3 o, d;
         camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
         store_path<kMode>(a.q, surv + j, o, d, p, s << kMetaDepthBits, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f, 0.0f);  // main.cpp:391
@@ -1227,7 +1224,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     if (emit) {
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
-        Pcg32 rng = path_rng(a.initstate, gpix, a.sample_jump[sample], a.cast_jump[depth]);
+        Pcg32 rng = path_rng(gpix, a.sample_jump[sample], a.cast_jump[depth]);
         const float t = hit.y, u = hit.z, v = hit.w;
         float xi_x, xi_y;
         draw2(rng, a.rng_order, xi_x, xi_y);                   // main.cpp:413
@@ -1396,9 +1393,7 @@ void render_fused_kernel(FusedArgs a) {
                     const uint32_t lx = pix % a.W, ly = pix / a.W;  // scanline (pixel blocks: refill_kernel only)
                     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
                     gpix = gy * a.W + lx;                          // main.cpp:379-382
-                    Pcg32 rng;
-                    rng.seed(a.initstate, (uint64_t)gpix);         // main.cpp:376
-                    rng.state = pcg_apply(a.sample_jump[sample], rng.state, rng.inc);
+                    Pcg32 rng = pcg_start(a.sample_jump[sample], (uint64_t)gpix);  // main.cpp:376 + the sample's draws
                     V3 o;
                     camera_ray(a.cam, rng, a.rng_order, lx, gy, o, dir);
                     rs = rng.state;

@@ -236,7 +236,7 @@ struct RefillArgs {
     uint32_t* surv_clear;       // zeroed by thread 0: the next shade's survivor counter (may be null)
     const uint32_t* casts_in;   // the preceding shade's queue count (null for a chunk's first refill):
                                 // thread 0 adds it and *surv to stats[0] / stats[1]
-    const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
+    const PcgJump* sample_jump; // [spp]: seeded, then s * (4 + 2D) draws on (pcg_seeded_jump)
     unsigned long long* stats;  // casts, continuations, regenerations
     uint32_t* exhausted;        // thread 0 writes iter_tag here when this refill starts the last work item
     uint32_t iter_tag;          // the host's iteration number + 2 (the chunk's first refill: 1)
@@ -302,7 +302,7 @@ struct ShadeArgs {
     uint32_t* count_out;        // survivors appended here (zeroed before the launch)
     float* sfilm;               // [spp_chunk][3][P]: one contribution per (sample, pixel) (albedo / emit)
     uint8_t* sflag;             // [spp_chunk][P]: escaped or not per (sample, pixel) (unit mode)
-    const PcgJump* sample_jump; // [spp]: jump by s * (4 + 2D) draws
+    const PcgJump* sample_jump; // [spp]: seeded, then s * (4 + 2D) draws on (pcg_seeded_jump)
     const PcgJump* cast_jump;   // [max_depth]: jump by 4 + 2 * cast draws
     uint64_t initstate;
     uint32_t P, W, sample0, max_depth, rr_start, rng_order;

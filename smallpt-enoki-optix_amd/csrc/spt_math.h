@@ -59,6 +59,20 @@ SPT_HD PcgJump pcg_jump_coeffs(uint64_t n) {
     return {acc_mul, acc_add};
 }
 SPT_HD uint64_t pcg_apply(PcgJump j, uint64_t state, uint64_t inc) { return j.mul * state + j.add * inc; }
+// seed(initstate S0, initseq) followed by jump j, as one affine map of the
+// stream constant inc = 2 initseq + 1: seed leaves state (inc + S0) M + inc,
+// the jump maps it to mul ((inc + S0) M + inc) + add inc = A inc + B with
+// A = mul (M + 1) + add and B = mul S0 M (mod 2^64) — one 64-bit multiply-add
+// per path start instead of three multiplies.  Stored as PcgJump {A, B}.
+SPT_HD PcgJump pcg_seeded_jump(uint64_t S0, PcgJump j) {
+    return {j.mul * (kPcgMult + 1u) + j.add, j.mul * S0 * kPcgMult};
+}
+SPT_HD Pcg32 pcg_start(PcgJump seeded, uint64_t initseq) {
+    Pcg32 r;
+    r.inc = (initseq << 1u) | 1u;
+    r.state = seeded.mul * r.inc + seeded.add;
+    return r;
+}
 
 // Real2C(next(), next()) — argument evaluation order is unspecified in the
 // reference (main.cpp:395,396,413); y-first = first draw to .y.

@@ -66,6 +66,29 @@ def test_pcg32_jump_ahead(n):
     assert (am * st + aa * inc) & M64 == s
 
 
+@pytest.mark.parametrize("seq", [0, 1, 1023, 2 ** 24 - 1])
+@pytest.mark.parametrize("n", [0, 4, 68, 63 * 68])
+def test_pcg32_seeded_jump_fold(seq, n):
+    """spt_math.h pcg_seeded_jump / pcg_start: seeding with initstate S0 and then
+    jumping n draws is one affine map of inc, A inc + B with A = mul (M + 1) +
+    add and B = mul S0 M: the draws that follow equal the oracle's sequential
+    PCG32 from draw n on."""
+    am, aa = _jump(n)
+    A = (am * (MULT + 1) + aa) & M64
+    B = (am * O.PCG32_DEFAULT_STATE * MULT) & M64
+    inc = ((seq << 1) | 1) & M64
+    st = (A * inc + B) & M64
+    out = []
+    for _ in range(6):  # pcg32 next_u32 (A1)
+        old = st
+        st = (old * MULT + inc) & M64
+        xs = (((old >> 18) ^ old) >> 27) & 0xFFFFFFFF
+        rot = old >> 59
+        out.append(((xs >> rot) | (xs << ((32 - rot) & 31))) & 0xFFFFFFFF)
+    np.testing.assert_array_equal(np.array(out, np.uint32),
+                                  O.pcg32_seq(O.PCG32_DEFAULT_STATE, seq, n + 6)[n:])
+
+
 def test_camera_known_answers():
     p = O.reference_params(1024, 1024, 1, 1)
     o, d, basis = O.camera_ray(p, 0, 0, [0, 0, 0, 0])
