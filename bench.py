@@ -409,6 +409,9 @@ def main():
         work_order = {1: "sample-major", 2: "pixel-major"}.get(st.get("work_order"), "?")
         if scene.backend.config["work_order"] == 0:
             work_order += " (auto)"
+        queue_cache = {0: None, 1: "cached", 2: "stream"}.get(st.get("queue_cache"), "?")
+        if queue_cache and scene.backend.config["queue_cache"] == 0:
+            queue_cache += " (auto)"
         launches = max(agg["isect_launches"], 1)
         avg_ms = agg["isect_ms"] / launches
         casts_per_launch = agg["ray_casts"] / launches
@@ -480,6 +483,8 @@ def main():
             "work_order_rule": "auto: pixel-major for scenes of >= 256 MiB, fused tiles of >= 16M paths and "
                                "wavefront tiles of <= 4M px over scenes of >= 4 MiB (24M paths in flight), "
                                "else sample-major (DESIGN.md §4)",
+            "queue_cache_rule": "auto: non-temporal path-queue / hit accesses for scenes of >= 256 MiB, else "
+                                "cached (DESIGN.md §4)",
             "pipeline_rule": "auto: fused for tiles of <= 32M paths, else wavefront (DESIGN.md §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
@@ -492,7 +497,7 @@ def main():
                                       if args.smallpt else ""),
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
                        "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(s_bar, 4),
-                       "work_order": work_order},
+                       "work_order": work_order, "queue_cache": queue_cache},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",

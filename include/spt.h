@@ -134,7 +134,7 @@ typedef struct spt_render_stats {
     uint64_t film_slots_unwritten; /* per-(sample, pixel) film slots still holding the pre-render
                                       sentinel when the resolve read them */
     uint32_t work_order;        /* the order that ran: SPT_WORK_SAMPLE_MAJOR or SPT_WORK_PIXEL_MAJOR */
-    uint32_t reserved0;
+    uint32_t queue_cache;       /* the queue caching that ran: SPT_QUEUE_CACHE_CACHED or _STREAM (0: fused) */
     uint64_t isect_tri_wave_steps;  /* SPT_FLAG_TRAVERSAL_STATS: wave steps in which some lane tested a triangle */
     uint64_t isect_node_wave_steps; /*   ... in which some lane visited a node */
     double isect_begin_ms, isect_end_ms; /* SPT_FLAG_TIMING: start of the first / end of the last isect launch
@@ -213,6 +213,11 @@ enum {
     SPT_WORK_SAMPLE_MAJOR = 1,
     SPT_WORK_PIXEL_MAJOR = 2
 };
+enum {
+    SPT_QUEUE_CACHE_AUTO = 0,
+    SPT_QUEUE_CACHE_CACHED = 1,   /* path-queue / hit accesses through the caches as usual */
+    SPT_QUEUE_CACHE_STREAM = 2    /* non-temporal: the caches stay with the BVH and triangles */
+};
 typedef struct spt_config {
     /* --- scene build (spt_scene_create_cfg) */
     uint32_t build;                 /* spt_build (AUTO: GPU from gpu_build_min_tris up)      [0..2] */
@@ -259,6 +264,12 @@ typedef struct spt_config {
                                        scenes of >= 4 MiB (then 24M paths in flight if
                                        wavefront_paths is left at 32M); the
                                        image does not depend on it                       [0..2] */
+    uint32_t queue_cache;           /* SPT_QUEUE_CACHE_*: how the wavefront's path-queue and hit
+                                       records (written once, read once per cast) use the
+                                       caches; AUTO: STREAM for scenes of >= 256 MiB on the
+                                       device (they overflow the Infinity Cache anyway: config 4
+                                       +1.7 %), CACHED otherwise (config 2 -3.7 % streamed:
+                                       DESIGN.md §4); the image does not depend on it     [0..2] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

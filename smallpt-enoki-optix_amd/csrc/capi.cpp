@@ -547,6 +547,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(pack_groups, 0, 2)
     CFG_RANGE(pixel_block, 0, 64)
     CFG_RANGE(work_order, 0, SPT_WORK_PIXEL_MAJOR)
+    CFG_RANGE(queue_cache, 0, SPT_QUEUE_CACHE_STREAM)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -930,6 +931,7 @@ void spt_default_config(spt_config* c) {
     c->pack_groups = 1;
     c->pixel_block = 0;
     c->work_order = SPT_WORK_AUTO;
+    c->queue_cache = SPT_QUEUE_CACHE_AUTO;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1712,6 +1714,14 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         cfg.work_order == SPT_WORK_PIXEL_MAJOR ||
         (cfg.work_order == SPT_WORK_AUTO && (scene_bytes >= kPixelMajorMinSceneBytes ||
                                              (fused && P * p.spp >= kPixelMajorMinFusedPaths) || wave_pm));
+    // Queue caching (spt_config.queue_cache).  AUTO: non-temporal path-queue
+    // and hit accesses for a scene beyond the Infinity Cache, so the caches
+    // keep BVH nodes and triangles (config 4 +1.7 %); cached otherwise, where
+    // the next kernel still finds the queue's lines (config 2 -3.7 %, config 3
+    // -0.7 % streamed; config 1 within noise: profiles/r04_exp2/).
+    const uint32_t queue_nt =
+        cfg.queue_cache == SPT_QUEUE_CACHE_STREAM ||
+        (cfg.queue_cache == SPT_QUEUE_CACHE_AUTO && scene_bytes >= kPixelMajorMinSceneBytes);
     if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
         C = kPixelMajorWavefrontPaths;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
@@ -1835,6 +1845,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         IsectQueueArgs& I = ia[k];
         I.sc = sc->dev();
         I.hits = (float4*)b.hits;
+        I.nt = queue_nt;
         I.max_depth = p.max_depth;
         I.trav_stats = trav_stats ? slot->dev->trav : nullptr;
         I.next = &b.cnt->isect_next;
@@ -1859,6 +1870,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         S.rr_start = p.rr_start_depth; S.rng_order = p.rng_order;
         S.tile_index = p.tile_index; S.tile_count = p.tile_count; S.rows_per_group = p.rows_per_group;
         S.work_order = pixel_major;
+        S.nt = queue_nt;
         S.env_r = p.env[0]; S.env_g = p.env[1]; S.env_b = p.env[2];
         RefillArgs& R = ra[k];
         R.cam = cam;
@@ -1868,6 +1880,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         R.tile_index = p.tile_index; R.tile_count = p.tile_count; R.rows_per_group = p.rows_per_group;
         R.pixel_block = cfg.pixel_block;
         R.work_order = pixel_major;
+        R.nt = queue_nt;
         R.initstate = p.rng_initstate;
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
@@ -2103,6 +2116,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     guard.armed = false;
     rs.iterations = iters;
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
+    rs.queue_cache = fused ? 0u : (queue_nt ? SPT_QUEUE_CACHE_STREAM : SPT_QUEUE_CACHE_CACHED);
     rs.streams = (uint32_t)K;
     rs.fused = fused ? 1u : 0u;
     slot->regen_base = std::min<uint64_t>(C, P * p.spp);

@@ -25,45 +25,49 @@ __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
 #endif
 }
 
-// Path-queue and hit-record accesses: each element is read or written once
-// per cast, so with SPT_NT_QUEUE they bypass cache retention (non-temporal)
-// and leave L2 / Infinity Cache to the BVH nodes and triangles.
-#ifndef SPT_NT_QUEUE
-#define SPT_NT_QUEUE 0
-#endif
+// Path-queue and hit-record accesses: each element is written once and read
+// once per cast.  kNt (spt_config.queue_cache): non-temporal, so they leave
+// L2 / Infinity Cache to the BVH nodes and triangles — a gain where the scene
+// itself overflows the Infinity Cache (config 4 +1.7 %), a loss where the
+// queue's lines would still be cached when the next kernel reads them
+// (config 2 -3.7 %, EXPERIMENTS.md round 4).
 typedef float spt_f4v __attribute__((ext_vector_type(4)));
 typedef float spt_f2v __attribute__((ext_vector_type(2)));
+template <bool kNt = false>
 __device__ __forceinline__ float4 ldq(const float4* p) {
-#if SPT_NT_QUEUE
-    const spt_f4v v = __builtin_nontemporal_load((const spt_f4v*)p);
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
+    if constexpr (kNt) {
+        const spt_f4v v = __builtin_nontemporal_load((const spt_f4v*)p);
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
 }
+template <bool kNt = false>
 __device__ __forceinline__ void stq(float4* p, float4 x) {
-#if SPT_NT_QUEUE
-    spt_f4v v = {x.x, x.y, x.z, x.w};
-    __builtin_nontemporal_store(v, (spt_f4v*)p);
-#else
-    *p = x;
-#endif
+    if constexpr (kNt) {
+        spt_f4v v = {x.x, x.y, x.z, x.w};
+        __builtin_nontemporal_store(v, (spt_f4v*)p);
+    } else {
+        *p = x;
+    }
 }
+template <bool kNt = false>
 __device__ __forceinline__ float2 ldq2(const float2* p) {
-#if SPT_NT_QUEUE
-    const spt_f2v v = __builtin_nontemporal_load((const spt_f2v*)p);
-    return make_float2(v.x, v.y);
-#else
-    return *p;
-#endif
+    if constexpr (kNt) {
+        const spt_f2v v = __builtin_nontemporal_load((const spt_f2v*)p);
+        return make_float2(v.x, v.y);
+    } else {
+        return *p;
+    }
 }
+template <bool kNt = false>
 __device__ __forceinline__ void stq2(float2* p, float2 x) {
-#if SPT_NT_QUEUE
-    spt_f2v v = {x.x, x.y};
-    __builtin_nontemporal_store(v, (spt_f2v*)p);
-#else
-    *p = x;
-#endif
+    if constexpr (kNt) {
+        spt_f2v v = {x.x, x.y};
+        __builtin_nontemporal_store(v, (spt_f2v*)p);
+    } else {
+        *p = x;
+    }
 }
 
 // minimum waves per SIMD the isect kernels are compiled for (register budget)
@@ -762,7 +766,7 @@ __device__ __forceinline__ void start_path(const RefillArgs& r, uint64_t w, V3& 
 #ifndef SPT_ISECT_CAM_WAVES
 #define SPT_ISECT_CAM_WAVES 8
 #endif
-template <typename Tr, bool kStats, bool kCam = false>
+template <typename Tr, bool kStats, bool kCam = false, bool kNt = false>
 __global__ __launch_bounds__(kIsectBlock)
 __attribute__((amdgpu_waves_per_eu(kStats ? 1 : (kCam ? SPT_ISECT_CAM_WAVES : Tr::kMinWaves), 8)))
 void isect_queue_kernel(IsectQueueArgs a) {
@@ -825,7 +829,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
                     V3 o, d;
                     uint32_t depth;
                     if (!kCam || ray < nq) {
-                        const float4 q1 = ldq(a.q.q1 + ray), q2 = ldq(a.q.q2 + ray);
+                        const float4 q1 = ldq<kNt>(a.q.q1 + ray), q2 = ldq<kNt>(a.q.q2 + ray);
                         o = v3(q1.x, q1.y, q1.z);
                         d = v3(q2.x, q2.y, q2.z);
                         depth = f2u(q1.w) & ((1u << kMetaDepthBits) - 1u);
@@ -833,10 +837,10 @@ void isect_queue_kernel(IsectQueueArgs a) {
                         // a new camera path: its ray is made here and stored for the shade
                         uint32_t p, meta;
                         start_path(a.cam, cur + (ray - nq), o, d, p, meta);
-                        stq(a.q.q1 + ray, make_float4(o.x, o.y, o.z, u2f(meta)));
-                        stq(a.q.q2 + ray, make_float4(d.x, d.y, d.z, u2f(p)));
-                        if (a.cam.mode >= kModeAlbedo) stq(a.q.q0 + ray, make_float4(1.0f, 1.0f, 1.0f, 0.0f));
-                        if (a.cam.mode == kModeEmit) stq2(a.q.rad + ray, make_float2(0.0f, 0.0f));
+                        stq<kNt>(a.q.q1 + ray, make_float4(o.x, o.y, o.z, u2f(meta)));
+                        stq<kNt>(a.q.q2 + ray, make_float4(d.x, d.y, d.z, u2f(p)));
+                        if (a.cam.mode >= kModeAlbedo) stq<kNt>(a.q.q0 + ray, make_float4(1.0f, 1.0f, 1.0f, 0.0f));
+                        if (a.cam.mode == kModeEmit) stq2<kNt>(a.q.rad + ray, make_float2(0.0f, 0.0f));
                         depth = 0;
                     }
                     // any-hit for the last cast unless emitters need the surface
@@ -844,7 +848,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
                     busy = !tr.finished();
                     if (!busy) {  // empty scene: the miss record init made
                         const TraceHit hh = tr.hit(a.sc, L);
-                        stq(a.hits + ray, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
+                        stq<kNt>(a.hits + ray, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
                     }
                 }
                 pool += take;
@@ -855,7 +859,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
         wave_steps++;
         if (busy && tr.step(a.sc, L, st)) {
             const TraceHit hh = tr.hit(a.sc, L);
-            stq(a.hits + ray, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
+            stq<kNt>(a.hits + ray, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
             busy = false;
         }
     }
@@ -985,13 +989,13 @@ __device__ __forceinline__ void camera_ray(const Camera& cam, Pcg32& rng, uint32
 }
 
 // A path's planes (PathQueue): the ray always, throughput / radiance as the mode needs.
-template <int kMode>
+template <int kMode, bool kNt = false>
 __device__ __forceinline__ void store_path(const PathQueue& q, uint32_t j, V3 o, V3 d, uint32_t pix, uint32_t meta,
                                            float tr, float tg, float tb, float lr, float lg, float lb) {
-    stq(q.q1 + j, make_float4(o.x, o.y, o.z, u2f(meta)));
-    stq(q.q2 + j, make_float4(d.x, d.y, d.z, u2f(pix)));
-    if (kMode >= kModeAlbedo) stq(q.q0 + j, make_float4(tr, tg, tb, kMode == kModeEmit ? lr : 0.0f));
-    if (kMode == kModeEmit) stq2(q.rad + j, make_float2(lg, lb));
+    stq<kNt>(q.q1 + j, make_float4(o.x, o.y, o.z, u2f(meta)));
+    stq<kNt>(q.q2 + j, make_float4(d.x, d.y, d.z, u2f(pix)));
+    if (kMode >= kModeAlbedo) stq<kNt>(q.q0 + j, make_float4(tr, tg, tb, kMode == kModeEmit ? lr : 0.0f));
+    if (kMode == kModeEmit) stq2<kNt>(q.rad + j, make_float2(lg, lb));
 }
 
 // PCG32 of global pixel gpix (main.cpp:376) advanced past the draws a path
@@ -1020,7 +1024,7 @@ __device__ __forceinline__ Pcg32 path_rng(uint32_t gpix, const PcgJump& js, cons
 #define SPT_REFILL_MAX_BLOCKS 4096
 #endif
 constexpr uint32_t kRefillMaxBlocks = SPT_REFILL_MAX_BLOCKS;
-template <int kMode>
+template <int kMode, bool kNt = false>
 __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
     const uint32_t surv = *a.surv;
     const uint64_t cur = a.cursor_in ? *a.cursor_in : a.cursor_init;
@@ -1058,7 +1062,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         Pcg32 rng = pcg_start(a.sample_jump[s], (uint64_t)gpix);  // main.cpp:376, then the sample's draws
         V3 o, d;
         camera_ray(a.cam, rng, a.rng_order, lx, gy, o, d);
-        store_path<kMode>(a.q, surv + j, o, d, p, s << kMetaDepthBits, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f, 0.0f);  // main.cpp:391
+        store_path<kMode, kNt>(a.q, surv + j, o, d, p, s << kMetaDepthBits, 1.0f, 1.0f, 1.0f, 0.0f, 0.0f, 0.0f);  // main.cpp:391
     }
 }
 
@@ -1076,7 +1080,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 // that work.
 // kSpt: the scene has smallpt spheres or mirror / glass materials (a separate
 // instance, so plain scenes keep the leaner register budget).
-template <int kMode, bool kSpt>
+template <int kMode, bool kSpt, bool kNt = false>
 __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
@@ -1106,12 +1110,12 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     }
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     if (i < n) {
-        const float4 q1 = ldq(a.in.q1 + i), q2 = ldq(a.in.q2 + i);
+        const float4 q1 = ldq<kNt>(a.in.q1 + i), q2 = ldq<kNt>(a.in.q2 + i);
         meta = f2u(q1.w);
         pix = f2u(q2.w);
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
-        hit = ldq(a.hits + i);
+        hit = ldq<kNt>(a.hits + i);
         slot = (int32_t)f2u(hit.x);
         if (kSpt && a.sc.nsph) {
             // smallpt's analytic spheres after the triangle BVH (the isect kernel
@@ -1124,11 +1128,11 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             hit = make_float4(u2f((uint32_t)slot), h.t, h.u, h.v);
         }
         if (kMode >= kModeAlbedo) {
-            const float4 q0 = ldq(a.in.q0 + i);
+            const float4 q0 = ldq<kNt>(a.in.q0 + i);
             tr = q0.x; tg = q0.y; tb = q0.z;
             if (kMode == kModeEmit) lr = q0.w;
         }
-        if (kMode == kModeEmit) { const float2 l = ldq2(a.in.rad + i); lg = l.x; lb = l.y; }
+        if (kMode == kModeEmit) { const float2 l = ldq2<kNt>(a.in.rad + i); lg = l.x; lb = l.y; }
         bool term = true, escaped = false;
         if (slot == -1) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
@@ -1251,7 +1255,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         }
     }
     __syncthreads();
-    if (emit) store_path<kMode>(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, tr, tg, tb, lr, lg, lb);
+    if (emit) store_path<kMode, kNt>(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, tr, tg, tb, lr, lg, lb);
 }
 
 // ------------------------------------------------------------ fused render
@@ -1585,7 +1589,7 @@ __global__ __launch_bounds__(256) void hit_info_kernel(HitInfoArgs a) {
 static inline uint32_t blocks_for(uint32_t items, uint32_t block) { return (items + block - 1) / block; }
 
 // Workgroups resident on the whole chip for this LDS stack size (cached).
-template <typename Tr, bool kStats, bool kCam>
+template <typename Tr, bool kStats, bool kCam, bool kNt>
 static uint32_t persistent_blocks(size_t lds) {
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
@@ -1594,7 +1598,7 @@ static uint32_t persistent_blocks(size_t lds) {
     (void)hipGetDevice(&dev);
     if (cached && cached_lds == lds && cached_dev == dev) return cached;
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<Tr, kStats, kCam>, kIsectBlock, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, isect_queue_kernel<Tr, kStats, kCam, kNt>, kIsectBlock, lds) !=
             hipSuccess || per_cu <= 0)
         per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
@@ -1604,19 +1608,22 @@ static uint32_t persistent_blocks(size_t lds) {
     return cached;
 }
 
-template <typename Tr, bool kStats, bool kCam = false>
+template <typename Tr, bool kStats, bool kCam = false, bool kNt = false>
 static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (grid_items == 0) return hipSuccess;
     const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
-    const uint32_t full = persistent_blocks<Tr, kStats, kCam>(lds);
+    const uint32_t full = persistent_blocks<Tr, kStats, kCam, kNt>(lds);
     const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)full * a.grid_q8) >> 8)) : full;
     const uint32_t blocks = min(scaled, blocks_for(grid_items, kIsectBlock));
-    hipLaunchKernelGGL((isect_queue_kernel<Tr, kStats, kCam>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
+    hipLaunchKernelGGL((isect_queue_kernel<Tr, kStats, kCam, kNt>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false>(a, grid_items, s);
+    if (a.nt)
+        return a.sc.node6 ? launch_isect_queue_t<Tracer6, false, false, true>(a, grid_items, s)
+                          : launch_isect_queue_t<Tracer8, false, false, true>(a, grid_items, s);
     return a.sc.node6 ? launch_isect_queue_t<Tracer6, false>(a, grid_items, s)
                       : launch_isect_queue_t<Tracer8, false>(a, grid_items, s);
 }
@@ -1683,6 +1690,12 @@ hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipSt
     if (grid_items == 0) return hipSuccess;
     const dim3 g(blocks_for(grid_items, kShadeBlock)), b(kShadeBlock);
     const bool spt = a.sc.nsph || a.sc.nkind;  // never in unit mode (spt_render)
+    if (a.nt && !spt) {  // non-temporal queue accesses (spt_config.queue_cache)
+        if (mode == kModeEmit) hipLaunchKernelGGL((shade_kernel<kModeEmit, false, true>), g, b, 0, s, a);
+        else if (mode == kModeAlbedo) hipLaunchKernelGGL((shade_kernel<kModeAlbedo, false, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((shade_kernel<kModeUnit, false, true>), g, b, 0, s, a);
+        return hipGetLastError();
+    }
     if (mode == kModeEmit && spt) hipLaunchKernelGGL((shade_kernel<kModeEmit, true>), g, b, 0, s, a);
     else if (mode == kModeEmit) hipLaunchKernelGGL((shade_kernel<kModeEmit, false>), g, b, 0, s, a);
     else if (mode == kModeAlbedo && spt) hipLaunchKernelGGL((shade_kernel<kModeAlbedo, true>), g, b, 0, s, a);
@@ -1739,7 +1752,11 @@ hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s
 #else
     const dim3 g(blocks_for(grid_items > 0 ? grid_items : 1, 256)), b(256);
 #endif
-    if (a.mode == kModeEmit) hipLaunchKernelGGL(refill_kernel<kModeEmit>, g, b, 0, s, a);
+    if (a.nt) {
+        if (a.mode == kModeEmit) hipLaunchKernelGGL((refill_kernel<kModeEmit, true>), g, b, 0, s, a);
+        else if (a.mode == kModeAlbedo) hipLaunchKernelGGL((refill_kernel<kModeAlbedo, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((refill_kernel<kModeUnit, true>), g, b, 0, s, a);
+    } else if (a.mode == kModeEmit) hipLaunchKernelGGL(refill_kernel<kModeEmit>, g, b, 0, s, a);
     else if (a.mode == kModeAlbedo) hipLaunchKernelGGL(refill_kernel<kModeAlbedo>, g, b, 0, s, a);
     else hipLaunchKernelGGL(refill_kernel<kModeUnit>, g, b, 0, s, a);
     return hipGetLastError();

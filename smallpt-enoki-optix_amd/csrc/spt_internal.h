@@ -248,6 +248,7 @@ struct RefillArgs {
     uint32_t chunk_s0, chunk_ns;  // the chunk's first sample and sample count
     uint64_t initstate;
     int mode;                   // PathMode: which planes a new path fills
+    uint32_t nt;                     // 1: non-temporal queue / hit accesses (spt_config.queue_cache)
 };
 
 struct IsectQueueArgs {
@@ -269,6 +270,7 @@ struct IsectQueueArgs {
     // (writing their rays for the shade) and does refill_kernel's bookkeeping
     // in block 0's first thread (cam.isect_next: the NEXT launch's counter).
     RefillArgs cam;
+    uint32_t nt;                     // 1: non-temporal queue / hit accesses (spt_config.queue_cache)
 };
 
 struct IsectPublicArgs {
@@ -310,6 +312,7 @@ struct ShadeArgs {
     uint32_t work_order, chunk_ns;  // film layout follows the work order (film_slot)
     float env_r, env_g, env_b;
     uint32_t xcd_remap;         // 1: blocks sharing an XCD take adjacent slot ranges
+    uint32_t nt;                     // 1: non-temporal queue / hit accesses (spt_config.queue_cache)
 };
 
 // Starts new paths in queue slots [*surv, capacity): work item w (sample-major:

@@ -40,6 +40,7 @@ EXPORTED = [
 SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
 SPT_WORK_AUTO, SPT_WORK_SAMPLE_MAJOR, SPT_WORK_PIXEL_MAJOR = 0, 1, 2
+SPT_QUEUE_CACHE_AUTO, SPT_QUEUE_CACHE_CACHED, SPT_QUEUE_CACHE_STREAM = 0, 1, 2
 
 
 class SptError(RuntimeError):
@@ -89,14 +90,12 @@ class RenderStats(ctypes.Structure):
                 ("fused", c_uint32), ("isect_busy_ms", c_double),
                 ("isect_max_stack", c_uint64),
                 ("paths_started", c_uint64), ("paths_terminated", c_uint64), ("film_slots_unwritten", c_uint64),
-                ("work_order", c_uint32), ("reserved0", c_uint32),
+                ("work_order", c_uint32), ("queue_cache", c_uint32),
                 ("isect_tri_wave_steps", c_uint64), ("isect_node_wave_steps", c_uint64),
                 ("isect_begin_ms", c_double), ("isect_end_ms", c_double)]
 
     def as_dict(self) -> dict:
-        d = {name: getattr(self, name) for name, _ in self._fields_}
-        d.pop("reserved0")
-        return d
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 class SceneStats(ctypes.Structure):
@@ -119,7 +118,7 @@ class Config(ctypes.Structure):
                 ("fused_refill_idle", c_uint32), ("fused_static_share_q8", c_uint32), ("fused_grid_q8", c_uint32),
                 ("plane_pad", c_uint32), ("film_budget_bytes", c_uint64),
                 ("public_persistent", c_uint32), ("public_refill_idle", c_uint32), ("pack_groups", c_uint32),
-                ("pixel_block", c_uint32), ("work_order", c_uint32)]
+                ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -241,6 +240,7 @@ _ENV_CONFIG = {
     "SPT_PACK": ("pack_groups", int),
     "SPT_PIXEL_BLOCK": ("pixel_block", int),
     "SPT_WORK_ORDER": ("work_order", int),
+    "SPT_QUEUE_CACHE": ("queue_cache", int),
 }
 
 

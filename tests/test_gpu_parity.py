@@ -320,6 +320,52 @@ def test_work_order_stream_shares(small, order):
     assert st["ray_casts"] == casts
 
 
+@pytest.mark.parametrize("cache", [1, 2])
+def test_queue_cache_bitexact(small, cache):
+    """spt_config.queue_cache (path-queue and hit records through the caches or
+    non-temporal) changes cache policy only: every shade mode (albedo +
+    roulette, emitters, unit) bit-equal to the oracle, and the stats name the
+    policy that ran."""
+    m, albedo, osc = small
+    w, h, spp, depth = 40, 30, 6, 4
+    cfg = sptamd.default_config()
+    cfg.queue_cache = cache
+    cfg.streams = 2
+    s = sptamd.Scene(config=cfg)
+    s.add_arrays(m)
+    s.commit(0)
+    s.backend.set_albedo(albedo)
+    got, st = render(s, w, h, spp, depth, pipeline="wavefront", wavefront_paths=3000, rr_start_depth=2)
+    ref, casts = osc.render(O.reference_params(w, h, spp, depth, rr_start_depth=2))
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts
+    assert st["queue_cache"] == cache
+    emi = np.zeros_like(albedo)
+    emi[1] = (0.5, 0.25, 0.125)
+    s.backend.set_emission(emi)
+    got_e, _ = render(s, w, h, spp, depth, pipeline="wavefront", wavefront_paths=3000)
+    ref_e, _ = O.OracleScene(m, albedo=albedo, emission=emi).render(O.reference_params(w, h, spp, depth))
+    np.testing.assert_array_equal(got_e, ref_e)
+    u = sptamd.Scene(config=cfg)
+    u.add_arrays(m)
+    u.commit(0)
+    got_u, st_u = render(u, w, h, spp, depth, pipeline="wavefront", wavefront_paths=3000)
+    ref_u, _ = O.OracleScene(m).render(O.reference_params(w, h, spp, depth))
+    np.testing.assert_array_equal(got_u, ref_u)
+    assert st_u["queue_cache"] == cache
+    # AUTO on this small scene (< 256 MiB on the device): cached
+    a = sptamd.Scene()
+    a.add_arrays(m)
+    a.commit(0)
+    got_a, st_a = render(a, w, h, spp, depth, pipeline="wavefront", wavefront_paths=3000)
+    np.testing.assert_array_equal(got_a, ref_u)
+    assert st_a["queue_cache"] == _lib.SPT_QUEUE_CACHE_CACHED
+    bad = sptamd.default_config()
+    bad.queue_cache = 3
+    assert _lib.lib.spt_scene_set_config(a.backend.handle, ctypes.byref(bad)) == 1
+    assert b"queue_cache" in _lib.lib.spt_last_error()
+
+
 def test_config_through_the_abi(small, monkeypatch):
     """Knobs set through spt_config (no environment variable anywhere) change
     scheduling only; invalid values are rejected by spt_scene_set_config."""
