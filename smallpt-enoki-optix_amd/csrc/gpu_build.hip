@@ -85,6 +85,22 @@ __global__ __launch_bounds__(kBlock) void tri_box_kernel(const float* __restrict
     else if (threadIdx.x < 6) atomicMax(&cb[threadIdx.x], s[threadIdx.x]);
 }
 
+// Morton codes of the triangle centroids on a cubic grid over the centroid
+// bounds (the longest axis's extent for all three: cells are cubes, so the
+// code's locality is the same along every axis).  Per-axis normalisation
+// gave the city's 20 x 5 x 16 extent 4x finer cells in y: its PLOC tree had a
+// 2.5 % higher SAH cost (96.6 vs 94.3) and rendered 1.4 % slower; a 4D code
+// with the box diagonal as the fourth coordinate (Vinkler et al. 2017) had
+// the same SAH and rendered 3.6 % slower (EXPERIMENTS.md round 4).
+#ifndef SPT_MORTON
+#define SPT_MORTON 1  // 0: per-axis normalised 63-bit, 1: cube-normalised 63-bit, 2: 4D (x, y, z, size) 60-bit
+#endif
+__device__ __forceinline__ uint64_t spread15_4(uint64_t x) {  // bit k of x to bit 4k
+    x &= 0x7fff;
+    uint64_t r = 0;
+    for (int k = 0; k < 15; k++) r |= ((x >> k) & 1ull) << (4 * k);
+    return r;
+}
 __global__ __launch_bounds__(kBlock) void morton_kernel(const float4* __restrict__ lo, const float4* __restrict__ hi,
                                                         uint32_t n, const uint32_t* __restrict__ cb,
                                                         uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
@@ -93,12 +109,23 @@ __global__ __launch_bounds__(kBlock) void morton_kernel(const float4* __restrict
     const float4 l = lo[i], h = hi[i];
     const float c[3] = {0.5f * (l.x + h.x), 0.5f * (l.y + h.y), 0.5f * (l.z + h.z)};
     uint64_t key = 0;
+    float cube = 0.0f;
+    for (int a = 0; a < 3; a++) cube = fmaxf(cube, ord2f(cb[3 + a]) - ord2f(cb[a]));
     for (int a = 0; a < 3; a++) {
         const float b0 = ord2f(cb[a]), b1 = ord2f(cb[3 + a]);
-        const float ext = b1 - b0;
+        const float ext = SPT_MORTON ? cube : b1 - b0;
         float t = ext > 0.0f ? (c[a] - b0) / ext : 0.5f;
         t = fminf(fmaxf(t, 0.0f), 1.0f);
-        key |= spread21((uint64_t)(t * 2097151.0f)) << (2 - a);
+        if (SPT_MORTON == 2) key |= spread15_4((uint64_t)(t * 32767.0f)) << (3 - a);
+        else key |= spread21((uint64_t)(t * 2097151.0f)) << (2 - a);
+    }
+    if (SPT_MORTON == 2) {
+        // the box diagonal as a fourth coordinate (Vinkler et al. 2017's
+        // extended Morton codes): large and small triangles part early
+        const float dx = h.x - l.x, dy = h.y - l.y, dz = h.z - l.z;
+        float sz = cube > 0.0f ? sqrtf(dx * dx + dy * dy + dz * dz) / (1.7320508f * cube) : 0.0f;
+        sz = fminf(fmaxf(sz, 0.0f), 1.0f);
+        key |= spread15_4((uint64_t)(sz * 32767.0f));
     }
     keys[i] = key;
     vals[i] = i;
