@@ -163,6 +163,8 @@ def test_config_defaults_and_env_overrides():
     assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 25      # spt.h docs = code
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
     assert c.pack_groups == 1
+    assert (c.work_order, c.queue_cache) == (_lib.SPT_WORK_AUTO, _lib.SPT_QUEUE_CACHE_AUTO)
+    assert sptamd.config_from_env(environ={"SPT_QUEUE_CACHE": "2"}).queue_cache == _lib.SPT_QUEUE_CACHE_STREAM
     e = sptamd.config_from_env(environ={"SPT_STREAMS": "2", "SPT_BUILD": "gpu", "SPT_FUSED": "0",
                                         "SPT_FILM_BUDGET": "1000", "SPT_COLLAPSE": "greedy", "SPT_BVH": "2"})
     assert (e.streams, e.build, e.pipeline, e.film_budget_bytes, e.collapse, e.bvh_width) == (2, 2, 1, 1000, 1, 2)
@@ -172,7 +174,8 @@ def test_config_defaults_and_env_overrides():
 
 @pytest.mark.parametrize("field,value", [("streams", 0), ("streams", 5), ("bvh_width", 4), ("ploc_radius", 12),
                                          ("isect_refill_idle", 65), ("film_budget_bytes", 0), ("pipeline", 3),
-                                         ("bvh_width", 7), ("pack_groups", 3)])
+                                         ("bvh_width", 7), ("pack_groups", 3), ("work_order", 3),
+                                         ("queue_cache", 3)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)
