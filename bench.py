@@ -25,14 +25,16 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "smallpt-enoki-optix_amd"))
 
-# Eight hardware queues per process (HIP's default, and the GPU box's setting, is
-# 4): the two working sets' sub-wavefront streams (four each, spt.h
-# spt_render_async) then run on queues of their own while consecutive renders
-# overlap (config 1 +1.9 %).  The HIP runtime reads it when it
-# starts, so it is set before torch is imported; SPT_HW_QUEUES overrides it.
-# The line records the value requested and the one the environment had.
+# Hardware queues per process: the environment's GPU_MAX_HW_QUEUES (HIP's
+# default and the GPU box's setting: 4) is what a library caller gets, so the
+# bench keeps it.  The library's default wavefront (two
+# sub-wavefront streams per working set, two sets: four streams, DESIGN.md
+# §6b) fits four queues.  SPT_HW_QUEUES overrides it for an experiment; the
+# HIP runtime reads it when it starts, so that happens before torch is
+# imported.  The line records the value in effect.
 HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
-os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SPT_HW_QUEUES", "8")
+if os.environ.get("SPT_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["SPT_HW_QUEUES"]
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_JSON = os.path.join(ROOT, "profiles", "isect_pmc.json")  # tools/pmc_isect.sh output

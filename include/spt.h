@@ -141,6 +141,8 @@ typedef struct spt_render_stats {
                                             (the fused kernel's launches in the fused pipeline), in ms from one
                                             clock per scene (the first timed render): renders queued back to
                                             back may overlap, and their union is the kernel's busy time */
+    uint64_t drained_paths;     /* wavefront: paths the drain launches finished (spt_config.drain_q8) */
+    uint64_t drain_launches;    /* wavefront: drain launches queued (each runs only if its queue is short) */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -270,6 +272,19 @@ typedef struct spt_config {
                                        device (they overflow the Infinity Cache anyway: config 4
                                        +1.7 %), CACHED otherwise (config 2 -3.7 % streamed:
                                        DESIGN.md §4); the image does not depend on it     [0..2] */
+    /* --- spt_render, the wavefront's drain */
+    uint32_t drain_q8;              /* once every work item of a sub-wavefront has started, a queue
+                                       holding fewer paths than drain_q8/256 of that stream's
+                                       persistent isect lanes is finished by one drain launch (each
+                                       lane continues its paths to termination) instead of one
+                                       isect + shade launch per cast; 0: off.  The image does not
+                                       depend on it                   [0..65535] */
+    uint32_t drain_grid_q8;         /* the drain's persistent grid in 1/256 of the chip,
+                                       0 = 256/streams                                  [0..4096] */
+    uint32_t drain_casts;           /* with drain_q8: the drain also runs, whatever the queue's
+                                       length, this many casts after the stream's last work
+                                       item started, and ends the stream's launches; 0: only
+                                       on a short queue                                  [0..64] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -618,6 +618,8 @@ static inline void wray_setup(wray* r) {
 #define BOX_PAD 1.000001f
 /* node culling runs 4e-6 below tmin (spt_math.h cull_tmin): a box culled there
  * holds only triangles the box-exit rule drops anyway */
+#define BOX_PAD_LO 0.999999f
+static inline float pad_up(float x) { return x * (x >= 0.0f ? BOX_PAD : BOX_PAD_LO); }
 #define CULL_TMIN_REL 4e-6f
 static inline float cull_tmin(float tmin) { return tmin - fabsf(tmin) * CULL_TMIN_REL; }
 static inline uint32_t fbits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
@@ -627,9 +629,11 @@ static inline float exit_offset(float a, float b, float c, float S, float Sz) {
     return neg ? -fminf(fminf(a, b), c) : fmaxf(fmaxf(a, b), c);
 }
 
-/* Returns 1 and t/u/v when the triangle is hit with t in [tmin, tmax]. */
-static inline int woop_test(const wray* r, const float* tv, float tmin, float tmax,
-                            float* t_out, float* u_out, float* v_out) {
+/* Returns 1 and t/u/v when the triangle is hit with t in [tmin, tmax].
+ * rule: 1 applies the box-exit rule (every tracer); 2 (oracle_box_rule_audit)
+ * returns 2 for a hit the rule drops, with t/u/v set. */
+static inline int woop_test_r(const wray* r, const float* tv, float tmin, float tmax,
+                              float* t_out, float* u_out, float* v_out, int rule) {
 #ifdef ORACLE_ALT_TRI
     /* Moller-Trumbore, barycentrics in the same p = (1-u-v) v0 + u v1 + v v2 convention */
     {
@@ -684,16 +688,22 @@ static inline int woop_test(const wray* r, const float* tv, float tmin, float tm
     /* Box-exit rule (spt_math.h left_box_before_tmin): the hit counts only if
      * the ray has not left the triangle's own box before tmin, so the closest
      * hit does not depend on the tree (wavefront_isect.cu:103).
-     * Per axis the exit t times kBoxPad against tmin, without a divide. */
-    if (fmaxf(fmaxf(Az, Bz), Cz) * BOX_PAD < tmin) return 0;
-    if ((ex * fabsf(r->Sz)) * BOX_PAD < tmin * fabsf(r->Sx)) return 0;
-    if ((ey * fabsf(r->Sz)) * BOX_PAD < tmin * fabsf(r->Sy)) return 0;
+     * Per axis the exit t padded toward +inf (x BOX_PAD, or x BOX_PAD_LO when
+     * negative: a negative tmin allows that) against tmin, without a divide. */
+    const int drop = rule && (pad_up(fmaxf(fmaxf(Az, Bz), Cz)) < tmin ||
+                              pad_up(ex * fabsf(r->Sz)) < tmin * fabsf(r->Sx) ||
+                              pad_up(ey * fabsf(r->Sz)) < tmin * fabsf(r->Sy));
+    if (drop && rule != 2) return 0;
     /* + 0.0f: a zero t, u or v is +0 (spt_math.h woop_core: its sign would
      * follow det's, which the kx / ky order flips) */
     *t_out = t + 0.0f;
     *u_out = V / det + 0.0f;
     *v_out = W / det + 0.0f;
-    return 1;
+    return drop ? 2 : 1;
+}
+static inline int woop_test(const wray* r, const float* tv, float tmin, float tmax,
+                            float* t_out, float* u_out, float* v_out) {
+    return woop_test_r(r, tv, tmin, tmax, t_out, u_out, v_out, 1);
 }
 
 /* Slab test over the closed box.  A direction component whose reciprocal is
@@ -709,7 +719,7 @@ static inline int box_test(const wray* r, const onode* nd, float tmin, float tma
         }
         float t0 = (nd->bmin[k] - r->o[k]) * r->inv[k];
         float t1 = (nd->bmax[k] - r->o[k]) * r->inv[k];
-        float lo = fminf(t0, t1), hi = fmaxf(t0, t1) * BOX_PAD;
+        float lo = fminf(t0, t1), hi = pad_up(fmaxf(t0, t1));  /* toward +inf, either sign */
         tn = fmaxf(tn, lo);
         tf = fminf(tf, hi);
     }
@@ -746,7 +756,7 @@ static void trace(const oscene* s, const wray* r, float tmin, float tmax, int cl
         /* the current hit padded like the exit planes: boxes entered at the
          * hit's t (ties at shared edges / vertices) are still visited; boxes
          * the ray leaves before cull_tmin(tmin) are culled, as on the GPU */
-        if (!box_test(r, nd, cull_tmin(tmin), h->t * BOX_PAD)) continue;
+        if (!box_test(r, nd, cull_tmin(tmin), pad_up(h->t))) continue;
         if (nd->count) {
             for (int32_t i = 0; i < nd->count; i++) {
                 consider(s, r, s->prims[nd->left + i], tmin, h);
@@ -856,6 +866,85 @@ void oracle_intersect(void* scene, const float* ox, const float* oy, const float
     isect_ctx c = {(const oscene*)scene, ox, oy, oz, dx, dy, dz, tmin, tmax, mask, mask_size,
                    tri_id, t, u, v, do_closest};
     parallel_for(n, 256, nthreads, isect_one, &c);
+}
+
+/* ------------------------------------------------ box-exit rule audit */
+/* Every (ray, triangle) pair whose Woop test accepts a t in [tmin, tmax] that
+ * the box-exit rule then drops (test infrastructure: tests/test_oracle.py and
+ * tests/test_gpu_configs.py check each against a float64 box exit).  The
+ * triangles are enumerated along the whole ray line — boxes grown by 1e-4 of
+ * their extent and position, nothing culled on the near side — so no culling
+ * decides which pairs are seen. */
+typedef struct {
+    const oscene* s;
+    const float *ox, *oy, *oz, *dx, *dy, *dz, *tmin, *tmax;
+    int64_t* ray; int32_t* tri; float* t;
+    int64_t cap;
+    atomic_llong found, accepted;
+} audit_ctx;
+static inline int line_box(const wray* r, const onode* nd, float tmax) {
+    float tn = -INFINITY, tf = tmax;
+    for (int k = 0; k < 3; k++) {
+        const float g = 1e-4f * ((nd->bmax[k] - nd->bmin[k]) + fmaxf(fabsf(nd->bmin[k]), fabsf(nd->bmax[k]))) + 1e-30f;
+        const float lo = nd->bmin[k] - g, hi = nd->bmax[k] + g;
+        if (isinf(r->inv[k])) {
+            if (r->o[k] < lo || r->o[k] > hi) return 0;
+            continue;
+        }
+        const float t0 = (lo - r->o[k]) * r->inv[k], t1 = (hi - r->o[k]) * r->inv[k];
+        tn = fmaxf(tn, fminf(t0, t1));
+        tf = fminf(tf, fmaxf(t0, t1) * 1.0001f + 1e-30f);
+    }
+    return tn <= tf;
+}
+static void audit_pair(audit_ctx* c, const wray* r, int64_t i, int32_t p) {
+    float t, u, v;
+    const int res = woop_test_r(r, &c->s->v[(int64_t)p * 9], c->tmin[i], c->tmax[i], &t, &u, &v, 2);
+    if (!res) return;
+    atomic_fetch_add(&c->accepted, 1);
+    if (res != 2) return;
+    const int64_t k = atomic_fetch_add(&c->found, 1);
+    if (k < c->cap) { c->ray[k] = i; c->tri[k] = p; c->t[k] = t; }
+}
+static void audit_one(void* c_, int64_t i) {
+    audit_ctx* c = (audit_ctx*)c_;
+    const oscene* s = c->s;
+    if (s->ntri <= 0) return;
+    wray r;
+    r.o[0] = c->ox[i]; r.o[1] = c->oy[i]; r.o[2] = c->oz[i];
+    r.d[0] = c->dx[i]; r.d[1] = c->dy[i]; r.d[2] = c->dz[i];
+    wray_setup(&r);
+    if (!s->use_bvh) {
+        for (int64_t p = 0; p < s->ntri; p++) audit_pair(c, &r, i, (int32_t)p);
+        return;
+    }
+    int32_t stack[256];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const onode* nd = &s->nodes[stack[--sp]];
+        if (!line_box(&r, nd, c->tmax[i])) continue;
+        if (nd->count) {
+            for (int32_t j = 0; j < nd->count; j++) audit_pair(c, &r, i, s->prims[nd->left + j]);
+        } else {
+            stack[sp++] = nd->left + 1;
+            stack[sp++] = nd->left;
+        }
+    }
+}
+int64_t oracle_box_rule_audit(void* scene, const float* ox, const float* oy, const float* oz, const float* dx,
+                              const float* dy, const float* dz, const float* tmin, const float* tmax, int64_t n,
+                              int64_t* out_ray, int32_t* out_tri, float* out_t, int64_t cap, int64_t* accepted,
+                              int32_t nthreads) {
+    audit_ctx c;
+    c.s = (const oscene*)scene;
+    c.ox = ox; c.oy = oy; c.oz = oz; c.dx = dx; c.dy = dy; c.dz = dz; c.tmin = tmin; c.tmax = tmax;
+    c.ray = out_ray; c.tri = out_tri; c.t = out_t; c.cap = cap;
+    atomic_init(&c.found, 0);
+    atomic_init(&c.accepted, 0);
+    parallel_for(n, 64, nthreads, audit_one, &c);
+    if (accepted) *accepted = (int64_t)atomic_load(&c.accepted);
+    return (int64_t)atomic_load(&c.found);
 }
 
 static inline uint32_t material_kind(const oscene* s, int32_t mat) {

@@ -103,9 +103,13 @@ struct Stats {
     unsigned long long trav[7];   // SPT_FLAG_TRAVERSAL_STATS: nodes, tris, lane steps, wave steps, max stack,
                                   // wave steps running the triangle block, the visit block
     unsigned long long unwritten; // film slots still holding the sentinel at resolve time
+    unsigned long long drained;   // paths finished by drain launches
 };
 
 constexpr int kMaxStreams = 4;
+// the drain phase starts when the host's (lagging) view of a stream's unstarted
+// work falls below this many queue capacities (spt_render_async)
+constexpr uint64_t kDrainLookahead = 6;
 
 // One render's own state, so that renders can be queued back to back
 // (spt_render_async) while earlier ones are still on the GPU: its device
@@ -175,6 +179,45 @@ struct WorkSet {
     }
 };
 
+// Before a scene mutator frees or replaces a device array that queued work may
+// still read (materials, textures, spheres, kinds): wait for every render of
+// both working sets (free_ev) and for the last public call on every stream
+// that made one (spt_intersect / spt_hit_info_compute, record_public_use).  The
+// caller holds the scene mutex, so nothing new is queued meanwhile.
+struct PublicUse {
+    hipStream_t stream;
+    hipEvent_t ev;
+};
+
+// The PCG32 jump table of one (spp, depth, seed) key: [spp] seeded sample maps,
+// then [depth] cast jumps (read-only while renders run).  A workspace keeps a
+// few, so a caller that changes the seed per render (progressive accumulation)
+// reuses them; a table is rewritten (on the render's stream, from its own
+// pinned staging copy) only after every render that read it has finished —
+// ev[s] is recorded after each render of working set s that used the table,
+// and a set's renders run in order — and a render on another stream waits
+// for the write (write_ev).  No device-wide synchronisation.
+constexpr int kJumpTables = 4;
+struct JumpTable {
+    PcgJump* dev = nullptr;
+    PcgJump* host = nullptr;            // pinned staging of the last write
+    size_t cap = 0;
+    uint32_t spp = 0, depth = 0;
+    uint64_t state = 0;
+    bool valid = false;
+    uint64_t lru = 0;
+    hipEvent_t write_ev = nullptr;
+    hipEvent_t ev[kWorkSets] = {};
+    bool ev_used[kWorkSets] = {};
+    void release() {
+        hfree(dev);
+        if (host) (void)hipHostFree(host);
+        if (write_ev) (void)hipEventDestroy(write_ev);
+        for (auto& e : ev) if (e) (void)hipEventDestroy(e);
+        *this = JumpTable();
+    }
+};
+
 struct Workspace {
     WorkSet sets[kWorkSets];
     // The working set of a render on caller stream `s`: the set bound to that
@@ -200,10 +243,8 @@ struct Workspace {
         lru->home = s;
         return *lru;
     }
-    size_t jump_cap = 0;
-    PcgJump* jumps = nullptr;           // [spp] sample jumps, then [kMaxDepthCasts] cast jumps (read-only)
-    uint32_t jump_key_spp = 0, jump_key_depth = 0;
-    uint64_t jump_key_state = 0;
+    JumpTable jt[kJumpTables];          // PCG32 jump tables for recent (spp, depth, seed) keys
+    uint64_t jt_clock = 0;
     RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
     uint64_t next_ticket = 1;
     hipEvent_t epoch = nullptr;         // the first timed render's time origin: isect_begin/end_ms count from it
@@ -216,7 +257,7 @@ struct Workspace {
     void release() {
         for (WorkSet& w : sets) w.release();
         if (epoch) (void)hipEventDestroy(epoch);
-        hfree(jumps);
+        for (JumpTable& t : jt) t.release();
         for (RenderSlot& r : slots) {
             hfree(r.dev);
             if (r.host) (void)hipHostFree(r.host);
@@ -267,6 +308,7 @@ struct spt_scene_t {
     uint32_t stack_depth = 1;
     spt_scene_stats stats{};
     Workspace ws;
+    std::vector<PublicUse> pub;  // streams of public calls, with an event after the last one (quiesce)
 
     DeviceScene dev() const {
         DeviceScene d;
@@ -278,6 +320,8 @@ struct spt_scene_t {
         return d;
     }
     void release() {
+        for (auto& u : pub) (void)hipEventDestroy(u.ev);
+        pub.clear();
         ws.release();
         hfree(nodes); hfree(nodes8); hfree(emission); hfree(tris); hfree(snrm); hfree(tc); hfree(orig2slot); hfree(albedo);
         hfree(tex_info); hfree(texels); hfree(spheres); hfree(sph_mat); hfree(mat_kind);
@@ -285,6 +329,36 @@ struct spt_scene_t {
 };
 
 namespace {
+
+// (see PublicUse) caller holds sc->mu
+spt_status quiesce_scene(spt_scene_t* sc) {
+    for (WorkSet& w : sc->ws.sets)
+        if (w.used && w.free_ev) HIP_TRY(hipEventSynchronize(w.free_ev));
+    for (auto& u : sc->pub) HIP_TRY(hipEventSynchronize(u.ev));
+    return SPT_OK;
+}
+
+// After a public call's launch on `s` (caller holds sc->mu).  At most 64
+// streams are tracked: beyond that the list is drained and restarted.
+spt_status record_public_use(spt_scene_t* sc, hipStream_t s) {
+    for (auto& u : sc->pub)
+        if (u.stream == s) {
+            HIP_TRY(hipEventRecord(u.ev, s));
+            return SPT_OK;
+        }
+    if (sc->pub.size() >= 64) {
+        for (auto& u : sc->pub) {
+            HIP_TRY(hipEventSynchronize(u.ev));
+            (void)hipEventDestroy(u.ev);
+        }
+        sc->pub.clear();
+    }
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    sc->pub.push_back({s, e});
+    HIP_TRY(hipEventRecord(e, s));
+    return SPT_OK;
+}
 
 spt_status ensure_device() {
     int n = 0;
@@ -377,32 +451,56 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
     return SPT_OK;
 }
 
-// The PCG32 jump table (shared by the sets, read-only while renders run): to
-// each sample's first draw, s * (4 + 2D), and from there to the bounce draw
-// of each cast, 4 + 2 * cast (main.cpp:395,396,413).  Rewritten only when
-// spp or depth change, after every queued render has finished with it.
-// [spp] per sample: seed(initstate, .) then the jump past s * (4 + 2D) draws,
-// as one affine map of the stream constant (spt_math.h pcg_seeded_jump);
-// then [depth] per cast: the jump past 4 + 2 cast draws.
-spt_status ensure_jumps(Workspace& w, uint32_t spp, uint32_t depth, uint64_t initstate) {
-    if (w.jumps && w.jump_key_spp == spp && w.jump_key_depth == depth && w.jump_key_state == initstate)
+// The PCG32 jump table of a render (JumpTable): to each sample's first draw,
+// s * (4 + 2D), and from there to the bounce draw of each cast, 4 + 2 * cast
+// (main.cpp:395,396,413).  [spp] per sample: seed(initstate, .) then the jump
+// past s * (4 + 2D) draws, as one affine map of the stream constant
+// (spt_math.h pcg_seeded_jump); then [depth] per cast: the jump past 4 + 2 cast
+// draws.  A hit costs nothing; a miss rewrites the least recently used table
+// on `stream` once the renders that read it are done.
+spt_status ensure_jumps(Workspace& w, hipStream_t stream, uint32_t spp, uint32_t depth, uint64_t initstate,
+                        JumpTable** out) {
+    JumpTable* t = nullptr;
+    for (JumpTable& x : w.jt)
+        if (x.valid && x.spp == spp && x.depth == depth && x.state == initstate) t = &x;
+    if (t) {
+        t->lru = ++w.jt_clock;
+        HIP_TRY(hipStreamWaitEvent(stream, t->write_ev, 0));  // written on another stream, perhaps
+        *out = t;
         return SPT_OK;
-    if (w.jumps) HIP_TRY(hipDeviceSynchronize());
-    const size_t n = (size_t)spp + kMaxDepthCasts;
-    if (n > w.jump_cap) {
-        hfree(w.jumps);
-        w.jump_cap = 0;
-        HIP_TRY(hipMalloc((void**)&w.jumps, sizeof(PcgJump) * n));
-        w.jump_cap = n;
     }
+    t = &w.jt[0];
+    for (JumpTable& x : w.jt)
+        if (!x.valid ? t->valid : x.lru < t->lru) t = &x;
+    for (int k = 0; k < kWorkSets; k++)
+        if (t->ev_used[k]) HIP_TRY(hipEventSynchronize(t->ev[k]));  // the renders that read it
+    if (t->write_ev) HIP_TRY(hipEventSynchronize(t->write_ev));     // and its last write (staging reuse)
+    t->valid = false;
+    const size_t n = (size_t)spp + kMaxDepthCasts;
+    if (n > t->cap) {
+        hfree(t->dev);
+        if (t->host) (void)hipHostFree(t->host);
+        t->host = nullptr;
+        t->cap = 0;
+        HIP_TRY(hipMalloc((void**)&t->dev, sizeof(PcgJump) * n));
+        HIP_TRY(hipHostMalloc((void**)&t->host, sizeof(PcgJump) * n, hipHostMallocDefault));
+        t->cap = n;
+    }
+    if (!t->write_ev) HIP_TRY(hipEventCreateWithFlags(&t->write_ev, hipEventDisableTiming));
+    for (auto& e : t->ev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const uint64_t per_sample = 4ull + 2ull * depth;
-    std::vector<PcgJump> jt((size_t)spp + depth);
-    for (uint32_t s = 0; s < spp; s++) jt[s] = pcg_seeded_jump(initstate, pcg_jump_coeffs((uint64_t)s * per_sample));
-    for (uint32_t j = 0; j < depth; j++) jt[(size_t)spp + j] = pcg_jump_coeffs(4ull + 2ull * j);
-    HIP_TRY(hipMemcpy(w.jumps, jt.data(), sizeof(PcgJump) * jt.size(), hipMemcpyHostToDevice));
-    w.jump_key_spp = spp;
-    w.jump_key_depth = depth;
-    w.jump_key_state = initstate;
+    for (uint32_t s = 0; s < spp; s++) t->host[s] = pcg_seeded_jump(initstate, pcg_jump_coeffs((uint64_t)s * per_sample));
+    for (uint32_t j = 0; j < depth; j++) t->host[(size_t)spp + j] = pcg_jump_coeffs(4ull + 2ull * j);
+    HIP_TRY(hipMemcpyAsync(t->dev, t->host, sizeof(PcgJump) * ((size_t)spp + depth), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipEventRecord(t->write_ev, stream));
+    for (bool& u : t->ev_used) u = false;
+    t->spp = spp;
+    t->depth = depth;
+    t->state = initstate;
+    t->valid = true;
+    t->lru = ++w.jt_clock;
+    *out = t;
     return SPT_OK;
 }
 
@@ -441,7 +539,7 @@ spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
     if (rs.tile_rows) {  // an empty tile queued nothing
         HIP_TRY(hipEventSynchronize(r.done));
         const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(r.host);
-        static_assert(sizeof(Stats) == 11 * sizeof(unsigned long long), "Stats is the 11 counters read back here");
+        static_assert(sizeof(Stats) == 12 * sizeof(unsigned long long), "Stats is the 12 counters read back here");
         rs.ray_casts = hstats[0];
         rs.continuations = hstats[1];
         rs.regenerations = hstats[2] > r.regen_base ? hstats[2] - r.regen_base : 0;
@@ -456,6 +554,7 @@ spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
         rs.film_slots_unwritten = hstats[10];
         rs.isect_tri_wave_steps = hstats[8];
         rs.isect_node_wave_steps = hstats[9];
+        rs.drained_paths = hstats[11];
         if (r.timing) {
             uint64_t nis = 0;
             std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin
@@ -548,6 +647,9 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(pixel_block, 0, 64)
     CFG_RANGE(work_order, 0, SPT_WORK_PIXEL_MAJOR)
     CFG_RANGE(queue_cache, 0, SPT_QUEUE_CACHE_STREAM)
+    CFG_RANGE(drain_q8, 0, 65535)
+    CFG_RANGE(drain_grid_q8, 0, 4096)
+    CFG_RANGE(drain_casts, 0, 64)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -877,6 +979,11 @@ spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t 
     HIP_TRY(hipMalloc((void**)&d, sizeof(float) * 3 * nmat));
     HIP_TRY(hipMemcpy(d, albedo_rgb, sizeof(float) * 3 * nmat, hipMemcpyHostToDevice));
     std::lock_guard<std::mutex> lk(sc->mu);
+    spt_status qs = quiesce_scene(sc);  // queued renders / calls may still read the old table
+    if (qs) {
+        hfree(d);
+        return qs;
+    }
     hfree(sc->albedo);
     sc->albedo = d;
     sc->nmat = nmat;
@@ -889,6 +996,8 @@ spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t 
 spt_status spt_scene_set_emission(spt_scene sc, const float* emission_rgb, uint32_t nmat) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_emission: NULL scene");
     std::lock_guard<std::mutex> lk(sc->mu);
+    spt_status qs = quiesce_scene(sc);  // queued renders may still read the old table
+    if (qs) return qs;
     hfree(sc->emission);
     sc->nemit = 0;
     if (!emission_rgb || nmat == 0) return SPT_OK;  // no emitters
@@ -932,6 +1041,9 @@ void spt_default_config(spt_config* c) {
     c->pixel_block = 0;
     c->work_order = SPT_WORK_AUTO;
     c->queue_cache = SPT_QUEUE_CACHE_AUTO;
+    c->drain_q8 = kDefaultDrainQ8;
+    c->drain_grid_q8 = 0;
+    c->drain_casts = kDefaultDrainCasts;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -962,6 +1074,8 @@ spt_status spt_scene_set_texture(spt_scene sc, uint32_t material, const float* r
         return fail(SPT_ERR_LIMIT, "spt_scene_set_texture: %u x %u texels exceeds 2^26", width, height);
     if (material >= (1u << 20)) return fail(SPT_ERR_LIMIT, "spt_scene_set_texture: material %u >= 2^20", material);
     std::lock_guard<std::mutex> lk(sc->mu);
+    spt_status qs = quiesce_scene(sc);  // queued renders may still read the old images (upload_textures frees them)
+    if (qs) return qs;
     if (material >= sc->tex_img.size()) {
         sc->tex_img.resize(material + 1);
         sc->tex_w.resize(material + 1, 0);
@@ -1019,6 +1133,8 @@ spt_status spt_scene_set_spheres(spt_scene sc, const float* center_radius, const
             return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: sphere %u radius must be finite and > 0", k);
     }
     std::lock_guard<std::mutex> lk(sc->mu);
+    spt_status qs = quiesce_scene(sc);  // queued renders / calls may still read the old spheres
+    if (qs) return qs;
     hfree(sc->spheres);
     hfree(sc->sph_mat);
     sc->nsph = 0;
@@ -1037,6 +1153,8 @@ spt_status spt_scene_set_material_kinds(spt_scene sc, const uint32_t* kinds, uin
     for (uint32_t i = 0; kinds && i < nmat; i++)
         if (kinds[i] > SPT_MAT_GLASS) return fail(SPT_ERR_INVALID, "spt_scene_set_material_kinds: kind %u of material %u", kinds[i], i);
     std::lock_guard<std::mutex> lk(sc->mu);
+    spt_status qs = quiesce_scene(sc);  // queued renders may still read the old kinds
+    if (qs) return qs;
     hfree(sc->mat_kind);
     sc->nkind = 0;
     bool any = false;
@@ -1086,6 +1204,10 @@ spt_status spt_bvh_build_stats(const float* tv, uint64_t ntri, const spt_config*
 
 spt_status spt_scene_destroy(spt_scene sc) {
     if (!sc) return SPT_OK;
+    {
+        std::lock_guard<std::mutex> lk(sc->mu);
+        (void)quiesce_scene(sc);  // nothing queued may still read what is freed
+    }
     sc->release();
     delete sc;
     return SPT_OK;
@@ -1585,12 +1707,6 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     if (mask && mask_size != 1 && mask_size != n)
         return fail(SPT_ERR_INVALID, "spt_intersect: mask_size %u must be 1 or n=%u", mask_size, n);
     IsectPublicArgs a;
-    {  // a consistent snapshot of the device arrays and knobs (the scene setters change them under mu)
-        std::lock_guard<std::mutex> lock(sc->mu);
-        a.sc = sc->dev();
-        a.refill_idle = sc->cfg.public_refill_idle;
-        a.persistent = sc->cfg.public_persistent;
-    }
     a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
     a.dx = rays->dx; a.dy = rays->dy; a.dz = rays->dz;
     a.tmin = rays->tmin; a.tmax = rays->tmax;
@@ -1598,8 +1714,15 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
     a.n = n;
     a.closest = do_closest;
+    // a consistent snapshot of the device arrays and knobs, launched and
+    // recorded under the mutex: a scene mutator waits for this launch before it
+    // frees an array the snapshot holds (quiesce_scene)
+    std::lock_guard<std::mutex> lock(sc->mu);
+    a.sc = sc->dev();
+    a.refill_idle = sc->cfg.public_refill_idle;
+    a.persistent = sc->cfg.public_persistent;
     HIP_TRY(launch_isect_public(a, (hipStream_t)stream));
-    return SPT_OK;
+    return record_public_use(sc, (hipStream_t)stream);
 }
 
 spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hits* hits, const uint8_t* mask,
@@ -1619,10 +1742,8 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: mask_size %u must be 1 or n=%u", mask_size, n);
     if (sc->ntri == 0 && sc->nsph == 0) return SPT_OK;
     HitInfoArgs a;
-    {
-        std::lock_guard<std::mutex> lock(sc->mu);
-        a.sc = sc->dev();
-    }
+    std::lock_guard<std::mutex> lock(sc->mu);  // as spt_intersect: launched and recorded under the mutex
+    a.sc = sc->dev();
     a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
     a.dx = rays->dx; a.dy = rays->dy; a.dz = rays->dz;
     a.tri_id = hits->tri_id; a.t = hits->t; a.u = hits->u; a.v = hits->v;
@@ -1634,7 +1755,7 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
     a.mat_id = out->mat_id;
     a.ntri = sc->ntri;
     HIP_TRY(launch_hit_info(a, (hipStream_t)stream));
-    return SPT_OK;
+    return record_public_use(sc, (hipStream_t)stream);
 }
 
 spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* film_dev, void* stream_,
@@ -1752,8 +1873,10 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     ws.last_ticket = sc->ws.next_ticket;
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P);
     if (st) return st;
-    if ((st = ensure_jumps(sc->ws, p.spp, p.max_depth, p.rng_initstate))) return st;
-    const PcgJump* jumps = sc->ws.jumps;
+    JumpTable* jtab = nullptr;
+    if ((st = ensure_jumps(sc->ws, stream, p.spp, p.max_depth, p.rng_initstate, &jtab))) return st;
+    const PcgJump* jumps = jtab->dev;
+    const int set_idx = (int)(&ws - sc->ws.sets);
     // HIP events around the isect launches (the roofline kernel); every other
     // launch only with SPT_FLAG_TIMING_ALL (each event pair costs host time).
     const bool timing = (p.flags & SPT_FLAG_TIMING) != 0;
@@ -1789,6 +1912,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     struct EnqueueGuard {
         WorkSet& ws;
         hipStream_t stream;
+        JumpTable& jt;
+        int set = 0;
         int K = 1;
         bool armed = true;
         ~EnqueueGuard() {
@@ -1798,9 +1923,11 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                 (void)hipStreamWaitEvent(stream, ws.sub[k].join_ev, 0);
             }
             (void)hipEventRecord(ws.free_ev, stream);
+            (void)hipEventRecord(jt.ev[set], stream);
+            jt.ev_used[set] = true;
             ws.used = true;
         }
-    } guard{ws, stream, K};
+    } guard{ws, stream, *jtab, set_idx, K};
     HIP_TRY(hipMemsetAsync(slot->dev, 0, sizeof(Stats), stream));
     // time origin for the isect launch intervals (their union = isect busy time)
     slot->timing = timing;
@@ -1837,6 +1964,12 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     IsectQueueArgs ia[kMaxStreams];
     ShadeArgs sa[kMaxStreams];
     RefillArgs ra[kMaxStreams];
+    FusedArgs da[kMaxStreams];   // the drain launches (launch_drain)
+    uint32_t drain_T[kMaxStreams] = {};
+    // the drain: not with traversal counters (isect kernel only) or camera
+    // paths started inside the isect launches (an experiment)
+    const bool drain_on = cfg.drain_q8 != 0 && !trav_stats && !kIsectCam;
+    uint64_t drain_launches = 0;
     PathQueue q[kMaxStreams][2];
     for (int k = 0; k < K; k++) {
         Sub& b = ws.sub[k];
@@ -1885,6 +2018,34 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
         R.exhausted = &b.cnt->exhausted;
+        I.drain_below = 0;
+        S.drain_below = 0;
+        if (drain_on) {
+            // a queue shorter than drain_q8/256 of this stream's isect lanes
+            drain_T[k] = (uint32_t)std::min<uint64_t>(
+                0xffffffffull, (uint64_t)isect_queue_lanes(I) * cfg.drain_q8 / 256u);
+            FusedArgs& D = da[k];
+            D = FusedArgs{};
+            D.sc = sc->dev();
+            D.cam = cam;
+            D.sample_jump = jumps;
+            D.cast_jump = jumps + p.spp;
+            D.sfilm = sfilm;
+            D.sflag = sflag;
+            D.stats = slot->dev->stats;
+            D.drained = &slot->dev->drained;
+            D.next = &b.cnt->isect_next;  // zeroed by the refill before; an isect that skips leaves it
+            D.initstate = p.rng_initstate;
+            D.P = (uint32_t)P; D.W = p.width; D.max_depth = p.max_depth;
+            D.rr_start = p.rr_start_depth; D.rng_order = p.rng_order;
+            D.tile_index = p.tile_index; D.tile_count = p.tile_count; D.rows_per_group = p.rows_per_group;
+            D.refill_idle = cfg.fused_refill_idle;
+            D.static_share_q8 = cfg.fused_static_share_q8;
+            D.chunk = cfg.isect_chunk;
+            D.grid_q8 = cfg.drain_grid_q8 ? cfg.drain_grid_q8 : 256u / (uint32_t)K;
+            D.env_r = p.env[0]; D.env_g = p.env[1]; D.env_b = p.env[2];
+            D.nt = queue_nt;
+        }
     }
 
     uint64_t iters = 0;
@@ -1950,6 +2111,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             HIP_TRY(hipMemsetAsync(b.cnt, 0, sizeof(Counters), strm[k]));
             ra[k].work_end = we;
             sa[k].sample0 = s0; sa[k].chunk_ns = ns;
+            da[k].sample0 = s0; da[k].pm_ns = pixel_major ? ns : 0;  // the shade's film layout
             // the first refill starts at the sub-wavefront's first work item
             ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = nullptr; ra[k].cursor_init = wb;
             ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];
@@ -2023,6 +2185,40 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         R.iter_tag = (uint32_t)it + 1;
                         ia[k].next = isect_next_of(b.cnt, c);
                     }
+                    // The drain phase: once the stream's last work items are (about
+                    // to be) started — the host's view lags one or two batches, in
+                    // which the cursor moves < kDrainLookahead capacities — a drain
+                    // launch follows the shade.  Whichever sees the queue short
+                    // (< drain_T) runs: the isect and shade skip and the drain
+                    // finishes every queued path, or the drain skips.  Later
+                    // iterations find the queue empty (no-op launches).
+                    const bool dph = drain_on && (limit[k] != UINT64_MAX ||
+                                                  sub_end[k] - started[k] < kDrainLookahead * (uint64_t)b.cap);
+                    // drain_casts after the exhausting refill (limit - max_depth) the
+                    // drain runs whatever the queue holds, and the stream ends: no
+                    // work is left to start, so nothing can enter its queue again
+                    const bool force = dph && cfg.drain_casts && limit[k] != UINT64_MAX &&
+                                       it + p.max_depth >= limit[k] + cfg.drain_casts;
+                    ia[k].drain_below = force ? 0xffffffffu : dph ? drain_T[k] : 0u;
+                    sa[k].drain_below = ia[k].drain_below;
+                    if (force) {
+                        da[k].q = q[k][c];
+                        da[k].qcount = &b.cnt->qn[c];
+                        da[k].drain_below = 0xffffffffu;
+                        if ((st = mark(1, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
+                        drain_launches++;
+                        // the refill's bookkeeping: the drained paths' first casts
+                        ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
+                        ra[k].cursor_out = &b.cnt->cursor[nx]; ra[k].qn_out = &b.cnt->qn[nx];
+                        ra[k].surv_clear = &b.cnt->surv[c];
+                        ra[k].casts_in = &b.cnt->qn[c];
+                        ra[k].iter_tag = (uint32_t)it + 2;
+                        if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], 0, strm[k]); }))) return st;
+                        cur[k] = nx;
+                        live[k] = false;
+                        nlive--;
+                        continue;
+                    }
                     if ((st = mark(1, strm[k], [&] {
                              return trav_stats ? launch_isect_queue_stats(ia[k], known[k], strm[k])
                                                : cam ? launch_isect_queue_cam(ia[k], known[k], strm[k])
@@ -2034,6 +2230,13 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                     sa[k].count_in = &b.cnt->qn[c];
                     sa[k].count_out = &b.cnt->surv[nx];
                     if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], mode, known[k], strm[k]); }))) return st;
+                    if (dph) {
+                        da[k].q = q[k][c];
+                        da[k].qcount = &b.cnt->qn[c];
+                        da[k].drain_below = drain_T[k];
+                        if ((st = mark(1, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
+                        drain_launches++;
+                    }
                     if (cam) {  // no refill launch: the next isect starts the new paths
                         cur[k] = nx;
                         continue;
@@ -2112,9 +2315,12 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     HIP_TRY(hipMemcpyAsync(slot->host, slot->dev, sizeof(Stats), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipEventRecord(slot->done, stream));
     HIP_TRY(hipEventRecord(ws.free_ev, stream));  // every sub-stream joined `stream` before the resolve
+    HIP_TRY(hipEventRecord(jtab->ev[set_idx], stream));  // this render is done with the jump table
+    jtab->ev_used[set_idx] = true;
     ws.used = true;
     guard.armed = false;
     rs.iterations = iters;
+    rs.drain_launches = drain_launches;
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
     rs.queue_cache = fused ? 0u : (queue_nt ? SPT_QUEUE_CACHE_STREAM : SPT_QUEUE_CACHE_CACHED);
     rs.streams = (uint32_t)K;

@@ -252,17 +252,18 @@ struct Tracer {
             slab(n0.z, n0.w, o.y, iy, b0, b1);
             slab(n2.x, n2.y, o.z, iz, c0, c1);
             const float tn0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), tbox));
-            const float tf0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1)) * kBoxPad;
+            // exits padded toward +inf (pad_up: a negative per-ray tmin allows negative exits)
+            const float tf0 = pad_up(fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fmaxf(c0, c1)));
             float d0, d1, e0, e1, f0, f1;
             slab(n1.x, n1.y, o.x, ix, d0, d1);
             slab(n1.z, n1.w, o.y, iy, e0, e1);
             slab(n2.z, n2.w, o.z, iz, f0, f1);
             const float tn1 = fmaxf(fmaxf(fminf(d0, d1), fminf(e0, e1)), fmaxf(fminf(f0, f1), tbox));
-            const float tf1 = fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1)) * kBoxPad;
+            const float tf1 = pad_up(fminf(fminf(fmaxf(d0, d1), fmaxf(e0, e1)), fmaxf(f0, f1)));
             // the current hit padded like the exit planes: a box entered at the
             // hit's t (a tie at a shared edge or vertex) is still visited, so
             // the smaller triangle id wins whatever the traversal order
-            const float th = h.t * kBoxPad;
+            const float th = pad_up(h.t);
             const bool h0 = tn0 <= fminf(tf0, th);
             const bool h1 = tn1 <= fminf(tf1, th);
             const int32_t ch0 = (int32_t)f2u(n3.x), ch1 = (int32_t)f2u(n3.y);
@@ -794,6 +795,7 @@ void isect_queue_kernel(IsectQueueArgs a) {
         }
     } else {
         n = *a.count;
+        if (n < a.drain_below) return;  // the drain launch after the shade takes this queue
     }
     typename std::conditional<kStats, TravStats, NoStats>::type st;
     Tr tr;
@@ -1086,6 +1088,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __shared__ uint32_t s_wave_off[kShadeBlock / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t n = *a.count_in;
+    if (n < a.drain_below) return;  // the drain launch takes this queue (launch_drain)
     // the grid may be sized from a stale (larger) count: remap only the
     // blocks that hold queued paths, so every XCD gets its eighth of them
     const uint32_t nreal = min(gridDim.x, (n + kShadeBlock - 1) / kShadeBlock);
@@ -1267,14 +1270,28 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 // refill_kernel) in the lanes that became free.  Path state never leaves the
 // registers, so there are no queues, compaction or per-bounce launches.  The
 // per-(sample, pixel) film writes are the same, so the image is bit-identical.
-template <typename Tr, int kMode>
+//
+// kDrain: the wavefront's drain (launch_drain).  The same lane loop, but a
+// free lane takes the next path of a wavefront queue — its ray, pixel,
+// sample and cast as the shade would read them, its PCG32 state re-derived at
+// its cast's bounce draw (path_rng) — instead of a new camera path, and
+// continues it to termination in registers.  Once a sub-wavefront's queue
+// falls below drain_below the per-cast launches (each ending in the latency
+// tail of its slowest ray) stop and one launch finishes every path.  Same
+// arithmetic, same film writes, so the same bits as the queue kernels.
+template <typename Tr, int kMode, bool kDrain = false, bool kNt = false>
 __global__ __launch_bounds__(kIsectBlock)
 __attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
-    const uint32_t n = a.count;
+    uint32_t n = a.count;
+    if constexpr (kDrain) {
+        n = wave_uniform(*a.qcount);
+        if (n >= a.drain_below) return;  // the isect and shade launches take this queue
+        if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(a.drained, (unsigned long long)n);
+    }
     NoStats st;
     Tr tr;
     V3 dir = v3(0, 0, 0);
@@ -1392,7 +1409,37 @@ void render_fused_kernel(FusedArgs a) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
-                if (!busy && !pending && rank < take) {
+                if (kDrain && !busy && !pending && rank < take) {
+                    // the next queued path (shade_kernel's reads), continued here
+                    const uint32_t j = pool + rank;
+                    const float4 q1 = ldq<kNt>(a.q.q1 + j), q2 = ldq<kNt>(a.q.q2 + j);
+                    const uint32_t meta = f2u(q1.w);
+                    depth = meta & ((1u << kMetaDepthBits) - 1u);
+                    sample = meta >> kMetaDepthBits;
+                    pix = f2u(q2.w);
+                    const uint32_t lx = pix % a.W, ly = pix / a.W;
+                    gpix = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group) * a.W + lx;
+                    dir = v3(q2.x, q2.y, q2.z);
+                    // at the bounce draw of this cast: 4 + 2 cast draws past the sample's first
+                    rs = path_rng(gpix, a.sample_jump[sample], a.cast_jump[depth]).state;
+                    thr = thg = thb = 1.0f;
+                    lr = lg = lb = 0.0f;
+                    if (kMode >= kModeAlbedo) {
+                        const float4 q0 = ldq<kNt>(a.q.q0 + j);
+                        thr = q0.x; thg = q0.y; thb = q0.z;
+                        if (kEmit) lr = q0.w;
+                    }
+                    if (kEmit) {
+                        const float2 l = ldq2<kNt>(a.q.rad + j);
+                        lg = l.x; lb = l.y;
+                    }
+                    tr.init(a.sc, v3(q1.x, q1.y, q1.z), dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit, L);
+                    busy = true;
+                    if (tr.finished()) {  // empty scene: a miss
+                        busy = false;
+                        pending = true;
+                    }
+                } else if (!kDrain && !busy && !pending && rank < take) {
                     work_item(pool + rank, a.sample0, a.pm_ns, a.P, a.pm_ns != 0, sample, pix);  // work0 = sample0 * P
                     const uint32_t lx = pix % a.W, ly = pix / a.W;  // scanline (pixel blocks: refill_kernel only)
                     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
@@ -1421,6 +1468,12 @@ void render_fused_kernel(FusedArgs a) {
             busy = false;
             pending = true;
         }
+    }
+    // the drain: a queued path's first cast here was counted with the queue
+    // (by the refill that follows), so only the casts after it are added
+    if constexpr (kDrain) {
+        casts = conts;
+        starts = 0;
     }
     // per-wave sums, one atomic per counter per wave
 #pragma unroll
@@ -1619,6 +1672,20 @@ static hipError_t launch_isect_queue_t(const IsectQueueArgs& a, uint32_t grid_it
     return hipGetLastError();
 }
 
+template <typename Tr, bool kNt>
+static uint32_t isect_queue_lanes_t(const IsectQueueArgs& a) {
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
+    const uint32_t full = persistent_blocks<Tr, false, false, kNt>(lds);
+    const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)full * a.grid_q8) >> 8)) : full;
+    return scaled * kIsectBlock;
+}
+
+uint32_t isect_queue_lanes(const IsectQueueArgs& a) {
+    if (!a.sc.nodes8) return isect_queue_lanes_t<Tracer, false>(a);
+    if (a.nt) return a.sc.node6 ? isect_queue_lanes_t<Tracer6, true>(a) : isect_queue_lanes_t<Tracer8, true>(a);
+    return a.sc.node6 ? isect_queue_lanes_t<Tracer6, false>(a) : isect_queue_lanes_t<Tracer8, false>(a);
+}
+
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false>(a, grid_items, s);
     if (a.nt)
@@ -1704,7 +1771,7 @@ hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipSt
     return hipGetLastError();
 }
 
-template <typename Tr, int kMode>
+template <typename Tr, int kMode, bool kDrain = false, bool kNt = false>
 static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* lanes_out) {
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
@@ -1714,8 +1781,8 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
     (void)hipGetDevice(&dev);
     if (!cached || cached_lds != lds || cached_dev != dev) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_fused_kernel<Tr, kMode>, kIsectBlock, lds) !=
-                hipSuccess || per_cu <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_fused_kernel<Tr, kMode, kDrain, kNt>,
+                                                         kIsectBlock, lds) != hipSuccess || per_cu <= 0)
             per_cu = 1;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
@@ -1724,10 +1791,29 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
         cached_dev = dev;
     }
     const uint32_t scaled = a.grid_q8 ? max(1u, (uint32_t)(((uint64_t)cached * a.grid_q8) >> 8)) : cached;
-    const uint32_t blocks = min(scaled, blocks_for(a.count > 0 ? a.count : 1, kIsectBlock));
+    // (the drain's grid cannot follow its count, which is on the device)
+    const uint32_t blocks = kDrain ? scaled : min(scaled, blocks_for(a.count > 0 ? a.count : 1, kIsectBlock));
     if (lanes_out) *lanes_out = blocks * kIsectBlock;
-    hipLaunchKernelGGL((render_fused_kernel<Tr, kMode>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
+    hipLaunchKernelGGL((render_fused_kernel<Tr, kMode, kDrain, kNt>), dim3(blocks), dim3(kIsectBlock), lds, s, a);
     return hipGetLastError();
+}
+
+template <int kMode, bool kNt>
+static hipError_t launch_drain_m(const FusedArgs& a, hipStream_t s) {
+    if (a.sc.nodes8 && a.sc.node6) return launch_fused_t<Tracer6F, kMode, true, kNt>(a, s, nullptr);
+    if (a.sc.nodes8) return launch_fused_t<Tracer8F, kMode, true, kNt>(a, s, nullptr);
+    return launch_fused_t<Tracer, kMode, true, kNt>(a, s, nullptr);
+}
+
+hipError_t launch_drain(const FusedArgs& a, int mode, hipStream_t s) {
+    if (a.nt) {
+        if (mode == kModeEmit) return launch_drain_m<kModeEmit, true>(a, s);
+        if (mode == kModeAlbedo) return launch_drain_m<kModeAlbedo, true>(a, s);
+        return launch_drain_m<kModeUnit, true>(a, s);
+    }
+    if (mode == kModeEmit) return launch_drain_m<kModeEmit, false>(a, s);
+    if (mode == kModeAlbedo) return launch_drain_m<kModeAlbedo, false>(a, s);
+    return launch_drain_m<kModeUnit, false>(a, s);
 }
 
 hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out) {

@@ -50,6 +50,12 @@ constexpr uint64_t kPixelMajorMinWaveSceneBytes = 4ull << 20;
 constexpr uint64_t kPixelMajorMaxWaveTilePx = 4ull << 20;
 constexpr uint32_t kDefaultWavefrontPaths = 1u << 25;
 constexpr uint64_t kPixelMajorWavefrontPaths = 24ull << 20;
+// spt_config.drain_q8 default: a sub-wavefront's queue shorter than this many
+// 1/256ths of its persistent isect lanes goes to the drain launch
+constexpr uint32_t kDefaultDrainQ8 = 512;
+// spt_config.drain_casts default: the drain runs this many casts after a
+// sub-wavefront's last work item started, whatever its queue holds
+constexpr uint32_t kDefaultDrainCasts = 3;
 
 // Path modes: what a path carries besides its ray.  The scene decides
 // (spt_render): unit = every albedo 1 and no emitters, the reference's own
@@ -263,6 +269,7 @@ struct IsectQueueArgs {
     uint32_t chunk;                  // dynamic chunk (rays per atomic)
     uint32_t grid_q8;                // persistent grid scale in 1/256ths of full occupancy (0 = full)
     uint32_t xcd_remap;              // 1: blocks sharing an XCD take adjacent static shares
+    uint32_t drain_below;            // skip the launch when *count < drain_below (launch_drain takes the queue)
     unsigned long long* trav_stats;  // non-null: nodes, tris, lane steps, wave steps
     // Camera paths started inside the launch (SPT_ISECT_CAMERA): the queue
     // holds cam.surv survivors in slots [0, surv); the launch starts
@@ -313,6 +320,7 @@ struct ShadeArgs {
     float env_r, env_g, env_b;
     uint32_t xcd_remap;         // 1: blocks sharing an XCD take adjacent slot ranges
     uint32_t nt;                     // 1: non-temporal queue / hit accesses (spt_config.queue_cache)
+    uint32_t drain_below;       // skip the launch when *count_in < drain_below (launch_drain takes the queue)
 };
 
 // Starts new paths in queue slots [*surv, capacity): work item w (sample-major:
@@ -336,6 +344,18 @@ struct FusedArgs {
                                 // one argument for both, the kernel is short of SGPRs
     uint32_t refill_idle, static_share_q8, chunk, grid_q8;
     float env_r, env_g, env_b;
+    // Drain mode (launch_drain): the same lane loop over the paths of a
+    // wavefront queue instead of new camera paths.  The launch runs only when
+    // *qcount < drain_below (else the isect and shade launches of the same
+    // iteration do); it takes queue slots [0, *qcount), continues every path
+    // in its lane to termination and adds to the stats only the casts after
+    // each path's first (the refill that follows counts the queue itself).
+    PathQueue q;
+    const uint32_t* qcount;
+    const PcgJump* cast_jump;       // [max_depth]: jump by 4 + 2 * cast draws
+    uint32_t drain_below;
+    uint32_t nt;                    // 1: non-temporal queue loads (spt_config.queue_cache)
+    unsigned long long* drained;    // paths the drain launches took over
 };
 
 struct HitInfoArgs {
@@ -410,6 +430,13 @@ hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items
 hipError_t launch_isect_queue_cam(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);
 hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* lanes_out);
+// The wavefront's drain: render_fused_kernel's lane loop over the paths of a
+// queue (FusedArgs drain fields); runs only when the queue holds fewer than
+// drain_below paths.  grid_q8 scales the chip-wide persistent grid.
+hipError_t launch_drain(const FusedArgs& a, int mode, hipStream_t s);
+// Lanes of the persistent isect grid a launch with these arguments gets (the
+// drain threshold is counted in them).
+uint32_t isect_queue_lanes(const IsectQueueArgs& a);
 hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipStream_t s);
 hipError_t launch_refill(const RefillArgs& a, uint32_t grid_items, hipStream_t s);
 // Both count the film slots still holding the pre-render sentinel (never

@@ -266,20 +266,25 @@ SPT_HD WoopShear woop_shear(const WoopRay& r, V3 p0, V3 p1, V3 p2) {
 // allow.  Per axis k the exit is E_k = (farthest vertex offset) / |d_k|:
 //   kz: E = max(Az, Bz, Cz)  (Az = Sz (v_kz - o_kz) is already in t units),
 //   kx: E = ex |Sz| / |Sx|   (|d_kx| = |Sx| / |Sz|), ky likewise,
-// tested as E * kBoxPad < tmin without a divide.  Each side has <= 4 ulps of
-// rounding, under kBoxPad's 8.4, so a hit whose exact box exit is >= tmin is
-// never dropped; and node culling runs at cull_tmin() (4e-6 below tmin) so a
-// box the tree culls holds only triangles this rule drops anyway.
+// tested as pad_up(E) < tmin without a divide.  Each side has <= 4 ulps of
+// rounding, under the pad's 8.4 (toward +inf: x kBoxPad when E >= 0, x
+// kBoxPadLo when E < 0, which a negative per-ray tmin allows), so a hit whose
+// exact box exit is >= tmin is never dropped; and node culling runs at
+// cull_tmin() (4e-6 below tmin) so a box the tree culls holds only triangles
+// this rule drops anyway.  For tmin > 0 the negative branch never decides
+// (E < 0 is below tmin either way), so the render's bits do not depend on it.
 #ifndef SPT_TRI_BOX_RULE
 #define SPT_TRI_BOX_RULE 1
 #endif
 constexpr float kCullTminRel = 4e-6f;
 SPT_HD float cull_tmin(float tmin) { return tmin - fabsf(tmin) * kCullTminRel; }
+constexpr float kBoxPadLo = 0.999999f;  // the pad for a negative exit (toward +inf)
+SPT_HD float pad_up(float x) { return x * (x >= 0.0f ? kBoxPad : kBoxPadLo); }
 SPT_HD bool left_box_before_tmin(const WoopRay& r, const WoopShear& w, float Az, float Bz, float Cz, float tmin) {
-    if (fmaxf(fmaxf(Az, Bz), Cz) * kBoxPad < tmin) return true;
+    if (pad_up(fmaxf(fmaxf(Az, Bz), Cz)) < tmin) return true;
     const float asz = fabsf(r.Sz);
-    if ((w.ex * asz) * kBoxPad < tmin * fabsf(r.Sx)) return true;
-    return (w.ey * asz) * kBoxPad < tmin * fabsf(r.Sy);
+    if (pad_up(w.ex * asz) < tmin * fabsf(r.Sx)) return true;
+    return pad_up(w.ey * asz) < tmin * fabsf(r.Sy);
 }
 
 // The same shear from vertices and origin already in (kx, ky, kz) order

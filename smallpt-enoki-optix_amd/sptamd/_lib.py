@@ -92,7 +92,8 @@ class RenderStats(ctypes.Structure):
                 ("paths_started", c_uint64), ("paths_terminated", c_uint64), ("film_slots_unwritten", c_uint64),
                 ("work_order", c_uint32), ("queue_cache", c_uint32),
                 ("isect_tri_wave_steps", c_uint64), ("isect_node_wave_steps", c_uint64),
-                ("isect_begin_ms", c_double), ("isect_end_ms", c_double)]
+                ("isect_begin_ms", c_double), ("isect_end_ms", c_double),
+                ("drained_paths", c_uint64), ("drain_launches", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -118,7 +119,8 @@ class Config(ctypes.Structure):
                 ("fused_refill_idle", c_uint32), ("fused_static_share_q8", c_uint32), ("fused_grid_q8", c_uint32),
                 ("plane_pad", c_uint32), ("film_budget_bytes", c_uint64),
                 ("public_persistent", c_uint32), ("public_refill_idle", c_uint32), ("pack_groups", c_uint32),
-                ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32)]
+                ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32),
+                ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -241,6 +243,9 @@ _ENV_CONFIG = {
     "SPT_PIXEL_BLOCK": ("pixel_block", int),
     "SPT_WORK_ORDER": ("work_order", int),
     "SPT_QUEUE_CACHE": ("queue_cache", int),
+    "SPT_DRAIN_Q8": ("drain_q8", int),
+    "SPT_DRAIN_GRID_Q8": ("drain_grid_q8", int),
+    "SPT_DRAIN_CASTS": ("drain_casts", int),
 }
 
 

@@ -70,3 +70,30 @@ def surface_rays(intersect, lo, hi, n, seed):
     tgt = lo[:, None] + (hi - lo)[:, None] * rng.random(p.shape)
     d2 = np.where(np.arange(p.shape[1]) % 2 == 0, rng.normal(size=p.shape), tgt - p).astype(np.float32)
     return p, d2
+
+
+def edge_leaving_rays(pos, pos_tri, n, seed):
+    """Adversarial rays for the box-exit rule: each starts at a
+    float32 point of a random triangle within 1e-6..1e-2 (barycentric) of one
+    edge and leaves across that edge nearly in the triangle's plane (normal
+    component 1e-8..1e-3, either side), so the triangle's own Woop t is
+    rounding noise while the ray leaves its box within ~tmin.  Returns (o, d),
+    (3, n) float32 each."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    pos = np.asarray(pos, np.float32)
+    pt = np.asarray(pos_tri, np.int64).reshape(-1, 3)
+    v = pos[pt[rng.integers(0, len(pt), n)]].astype(np.float64)
+    b = rng.dirichlet([1, 1, 1], n)
+    b[:, 0] = 10 ** rng.uniform(-6, -2, n)
+    b[:, 1:] *= (1 - b[:, :1]) / b[:, 1:].sum(1, keepdims=True)
+    p = (v[:, 0] * b[:, :1] + v[:, 1] * b[:, 1:2] + v[:, 2] * b[:, 2:3]).astype(np.float32)
+    nrm = np.cross(v[:, 1] - v[:, 0], v[:, 2] - v[:, 0])
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True) + 1e-30
+    e = v[:, 2] - v[:, 1]
+    e /= np.linalg.norm(e, axis=1, keepdims=True) + 1e-30
+    out = np.cross(e, nrm)                     # in-plane, across the edge v1 v2 ...
+    out *= np.sign(np.einsum("ij,ij->i", out, v[:, 1] - v[:, 0]))[:, None]  # ... away from v0
+    s = np.sign(rng.uniform(-1, 1, n)) * 10 ** rng.uniform(-8, -3, n)
+    d = (out + rng.normal(size=(n, 1)) * 0.3 * e + s[:, None] * nrm).astype(np.float32)
+    return np.ascontiguousarray(p.T), np.ascontiguousarray(d.T)

@@ -187,3 +187,26 @@ def test_config4_known_ray_and_surface_rays_tree_independent():
     assert h.mean() > 0.3
     for x, y in zip(g[1:], b[1:]):
         np.testing.assert_array_equal(x[h], y[h])
+
+
+def test_config4_box_exit_rule_against_float64():
+    """VERDICT r4 item 5 on config 4's city (10M triangles, the scene where the
+    rule mattered): on the 2M+ rays leaving its surfaces and 1M adversarial
+    edge-leaving rays, every Woop hit the box-exit rule drops has a float64
+    box exit before tmin — no genuine hit in [tmin, tmax] is dropped
+    (test_oracle.box_exit_audit, the oracle's enumeration along the whole ray
+    line; the rule is the same code as the kernels', spt_math.h
+    left_box_before_tmin)."""
+    from conftest import edge_leaving_rays
+    from test_oracle import box_exit_audit
+    cfg, s, kw, alb, emi = setup(4)
+    osc = oracle_scene(4)
+    pos = np.asarray(s.mesh["pos"], np.float32)
+    so, sd = surface_rays(lambda o, d: osc.intersect(o, d, nthreads=16), pos.min(0), pos.max(0), 4_000_000, seed=3)
+    found, accepted, worst = box_exit_audit(s.mesh["pos"], s.mesh["pos_tri"], osc, so, sd)
+    print(f"city surface rays {so.shape[1]}: Woop hits {accepted}, dropped {found}, max exit/tmin {worst:.4f}")
+    assert so.shape[1] > 1_000_000
+    eo, ed = edge_leaving_rays(s.mesh["pos"], s.mesh["pos_tri"], 1_000_000, seed=7)
+    found2, accepted2, worst2 = box_exit_audit(s.mesh["pos"], s.mesh["pos_tri"], osc, eo, ed)
+    print(f"city edge-leaving rays {eo.shape[1]}: Woop hits {accepted2}, dropped {found2}, max exit/tmin {worst2:.4f}")
+    assert found + found2 > 0

@@ -214,6 +214,26 @@ def test_bvh_equals_bruteforce_on_surface_leaving_rays():
     assert o.shape[1] > 8000 and (a[0] >= 0).sum() > 500
 
 
+def test_golden_regenerations_recorded():
+    """every file a regeneration replaced is kept beside the
+    current one; the current vectors differ from each by exactly the counts
+    tests/golden/regen_log.json records, all within SURVEY §8(c)'s tolerance
+    (make_golden.compare), so a silent regeneration fails here."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(GOLDEN))
+    import make_golden as MG
+    log = json.load(open(os.path.join(os.path.dirname(GOLDEN), "regen_log.json")))
+    kept = MG.kept_files()
+    assert kept, "no replaced golden file kept"
+    cur = np.load(GOLDEN)
+    for f in kept:
+        res = MG.compare(np.load(os.path.join(os.path.dirname(GOLDEN), f)), cur)
+        assert all(v["ok"] for v in res.values()), (f, res)
+        changed = {k: v["changed"] for k, v in res.items() if v["changed"]}
+        assert f in log and log[f]["changed"] == changed, (f, changed)
+
+
 def test_golden_vectors():
     g = np.load(GOLDEN)
     for s, row in zip(g["pcg_seeds"], g["pcg_u32"]):
@@ -487,3 +507,94 @@ def test_box_exit_rule_keeps_hits_on_axis_aligned_triangles():
     clear = (np.abs(yw) < 0.999) & (np.abs(zw) < 0.999) & (tw > 0.0011) & (tw < tf * 0.999)
     assert clear.sum() > 1000
     assert np.all(np.isin(brute[0][clear], [0, 1])), "a clear wall hit was dropped"
+
+
+def test_box_exit_rule_keeps_hits_at_negative_tmin():
+    """ADVICE r4: with a negative per-ray tmin a box exit can be negative too;
+    the rule pads it toward +inf (spt_math.h pad_up), so a genuine hit whose
+    exact exit equals tmin is kept.  A wall z = -1 behind the origin, rays
+    along +z with tmin = -1: the hit at t = -1 is exact (its box exit is
+    exactly -1), and so is one at tmin = -0.5 - ... (the wall at t = -0.5)."""
+    pos = np.array([[-1, -1, -1], [1, -1, -1], [1, 1, -1], [-1, 1, -1]], np.float32)
+    m = {"pos_tri": np.array([[0, 1, 2], [0, 2, 3]], np.int32), "pos": pos}
+    n = 64
+    rng = np.random.default_rng(2)
+    o = np.stack([rng.uniform(-0.5, 0.5, n), rng.uniform(-0.5, 0.5, n), np.zeros(n)]).astype(np.float32)
+    d = np.stack([np.zeros(n), np.zeros(n), np.ones(n)]).astype(np.float32)
+    for scale in (1.0, 2.0):  # d = (0, 0, 1) hits at t = -1; d = (0, 0, 2) at t = -0.5
+        dd = d * np.float32(scale)
+        tmin = np.full(n, -1.0 / scale, np.float32)
+        for use_bvh in (False, True):
+            tri, t, _, _ = O.OracleScene(m, use_bvh=use_bvh).intersect(o, dd, tmin=tmin)
+            assert np.all(tri >= 0), (scale, use_bvh)
+            np.testing.assert_array_equal(t, tmin)
+        # just past the exit (tmin above it) the wall is not hit
+        tmin2 = np.full(n, np.nextafter(np.float32(-1.0 / scale), np.float32(1.0)), np.float32)
+        assert np.all(O.OracleScene(m, use_bvh=False).intersect(o, dd, tmin=tmin2)[0] == -1)
+
+
+def box_exit_audit(mesh_pos, pos_tri, sc, o, d, tmin=0.001):
+    """Every Woop hit in [tmin, tmax] that the box-exit rule drops
+    (oracle_box_rule_audit, enumerating triangles along the whole ray line)
+    against a float64 box exit: the exact exit of a dropped hit's triangle box
+    must lie before tmin — so no genuine hit (whose point lies in the box at
+    t >= tmin) is dropped.  Returns (dropped pairs, accepted pairs, the
+    largest exit / tmin ratio among the dropped)."""
+    import ctypes
+    n = o.shape[1]
+    lib = sc.lib
+    lib.oracle_box_rule_audit.restype = ctypes.c_int64
+    vp = ctypes.c_void_p
+    lib.oracle_box_rule_audit.argtypes = [vp] + [vp] * 8 + [ctypes.c_int64, vp, vp, vp, ctypes.c_int64, vp, ctypes.c_int32]
+    o = np.ascontiguousarray(o, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    tmn = np.full(n, tmin, np.float32)
+    tmx = np.full(n, 1e20, np.float32)
+    cap = 1 << 20
+    ray = np.zeros(cap, np.int64)
+    tri = np.zeros(cap, np.int32)
+    tt = np.zeros(cap, np.float32)
+    acc = ctypes.c_int64(0)
+    p = lambda a: a.ctypes.data  # noqa: E731
+    found = lib.oracle_box_rule_audit(sc.h, p(o[0]), p(o[1]), p(o[2]), p(d[0]), p(d[1]), p(d[2]), p(tmn), p(tmx), n,
+                                      p(ray), p(tri), p(tt), cap, ctypes.byref(acc), 8)
+    assert found <= cap
+    ray, tri = ray[:found], tri[:found]
+    v = np.asarray(mesh_pos, np.float64)[np.asarray(pos_tri, np.int64)[tri]]  # (k, 3 vertices, 3)
+    lo, hi = v.min(axis=1), v.max(axis=1)
+    oo, dd = o[:, ray].T.astype(np.float64), d[:, ray].T.astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        far = np.where(dd > 0, hi, lo)
+        ex = np.where(dd != 0, (far - oo) / dd, np.inf)
+        # a zero direction component: inside the slab for every t, or never
+        inside = (oo >= lo) & (oo <= hi)
+        ex = np.where((dd == 0) & ~inside, -np.inf, ex)
+    exit64 = ex.min(axis=1)
+    worst = float((exit64 / tmin).max()) if found else 0.0
+    assert np.all(exit64 < tmin), f"{int((exit64 >= tmin).sum())} dropped hits with a float64 box exit >= tmin"
+    return found, int(acc.value), worst
+
+
+def test_box_exit_rule_against_float64_on_surface_rays():
+    """the one leg of the parity argument that is not
+    lockstep.  On ~2M rays leaving mitsuba_synth's surfaces (conftest
+    surface_rays: origins on or next to triangle planes, both hemispheres)
+    every Woop hit the rule drops has a float64 box exit before tmin, so no
+    genuine hit in [tmin, tmax] is dropped (test_gpu_configs runs the same
+    audit on config 4's city).  The rule acts on none of those rays here, so
+    1M adversarial rays (conftest.edge_leaving_rays: leaving a triangle across
+    an edge, nearly in its plane) make the audit non-vacuous."""
+    from conftest import edge_leaving_rays, surface_rays
+    mesh = scenes.mitsuba_synth(detail=0.25)
+    sc = O.OracleScene(mesh, use_bvh=True)
+    pos = np.asarray(mesh["pos"], np.float32)
+    o, d = surface_rays(lambda o, d: sc.intersect(o, d), pos.min(0), pos.max(0), 2_000_000, seed=23)
+    found, accepted, worst = box_exit_audit(mesh["pos"], mesh["pos_tri"], sc, o, d)
+    print(f"surface rays {o.shape[1]}: Woop hits {accepted}, dropped by the rule {found} "
+          f"(largest float64 exit / tmin among them {worst:.4f})")
+    assert o.shape[1] > 500_000 and accepted > 100_000
+    o, d = edge_leaving_rays(mesh["pos"], mesh["pos_tri"], 1_000_000, seed=5)
+    found2, accepted2, worst2 = box_exit_audit(mesh["pos"], mesh["pos_tri"], sc, o, d)
+    print(f"edge-leaving rays {o.shape[1]}: Woop hits {accepted2}, dropped by the rule {found2} "
+          f"(largest float64 exit / tmin among them {worst2:.4f})")
+    assert found2 > 0  # the rule acts on these, and every drop was before tmin

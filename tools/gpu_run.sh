@@ -57,6 +57,10 @@ for s in "$@"; do
     trav4) run trav4 600 python tools/trav_stats.py --city --depths 8 --spp 8 ;;
     trav4h) run trav4h 600 env SPT_BUILD=host python tools/trav_stats.py --city --depths 8 --spp 8 ;;
     bench4h) run bench4h 600 env SPT_BUILD=host python bench.py --config 4 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    proftile2|proftile4|proftile8) n=${s#proftile}; run $s 400 rocprofv3 --kernel-trace --stats -d gpurun_out/$s -o run --output-format csv -- python tools/tile_sim.py --tiles $n --steps 4 --pipeline ${PIPE:-wavefront} ;;
+    drainsweep) for dq in ${DRAINS:-0 256 512 1024 2048}; do run drain$dq 300 env SPT_DRAIN_Q8=$dq python tools/tile_sim.py --tiles 1 2 4 8 --pipeline wavefront --steps 8; done ;;
+    sweep) run sweep 600 python tools/tile_sim.py --tiles ${TILES:-1 2 4 8} --pipeline ${PIPE:-wavefront} --steps ${STEPS:-8} --sweep $SWEEP ;;
+    matrix) i=0; IFS=';' read -ra CFGS <<< "$MATRIX"; for c in "${CFGS[@]}"; do i=$((i+1)); run matrix$i 300 env ${c//,/ } python tools/tile_sim.py --tiles ${TILES:-1 2 4 8} --pipeline ${PIPE:-wavefront} --steps ${STEPS:-40} --sweep REP=${REPS:-1,2} TAG=m$i; done ;;
     tilesimw) run tilesimw 400 python tools/tile_sim.py --tiles 1 2 4 8 --pipeline wavefront --timing ;;
     tilesima) run tilesima 400 python tools/tile_sim.py --tiles 1 2 4 8 --timing ;;
     tilesim) run tilesim 400 python tools/tile_sim.py ;;

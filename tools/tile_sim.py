@@ -27,7 +27,13 @@ def main():
     ap.add_argument("--timing", action="store_true", help="HIP events around every launch (as bench.py)")
     ap.add_argument("--wavefront", type=int, default=0, help="paths in flight (0 = the library default)")
     ap.add_argument("--sync", action="store_true", help="spt_render per step (no queued renders)")
+    ap.add_argument("--sweep", nargs="*", default=[],
+                    help="SPT_* knobs to sweep in this process, e.g. SPT_STREAMS=1,2,4 SPT_DRAIN_Q8=256,512 "
+                         "(every combination, each tile count)")
     args = ap.parse_args()
+    import itertools
+    axes = [(kv.split("=", 1)[0], kv.split("=", 1)[1].split(",")) for kv in args.sweep]
+    combos = list(itertools.product(*[v for _, v in axes])) or [()]
     import torch
 
     import bench
@@ -48,9 +54,19 @@ def main():
         scene.backend.set_albedo(a)
         scene.backend.set_emission(e)
     W, H, spp, D = cfg["width"], cfg["height"], cfg["spp"], cfg["depth"]
+    for combo in combos:
+        env = {name: val for (name, _), val in zip(axes, combo)}
+        os.environ.update(env)
+        run_tiles(args, scene, cfg, kw, W, H, spp, D, env)
+
+
+def run_tiles(args, scene, cfg, kw, W, H, spp, D, env):
+    import torch
+
+    import sptamd
     for n in args.tiles:
         p = sptamd.make_params(W, H, spp, D, tile_index=0, tile_count=n, rows_per_group=args.rows_per_group,
-                               timing=args.timing, pipeline=args.pipeline,
+                               timing=args.timing, pipeline=None if args.pipeline in (None, "auto") else args.pipeline,
                                wavefront_paths=args.wavefront, **kw)
         rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
         films = [torch.empty((3, rows, W), dtype=torch.float32, device="cuda") for _ in range(2)]
@@ -72,7 +88,12 @@ def main():
         rate = paths / dt / 1e6
         print(json.dumps({"tiles": n, "tile_rows": rows, "ms_per_step": round(dt * 1e3, 3),
                           "tile_mpaths_s": round(rate, 1), "projected_job_mpaths_s": round(rate * n, 1),
-                          "iterations": st["iterations"], "fused": st["fused"]}), flush=True)
+                          "iterations": st["iterations"], "fused": st["fused"], "streams": st["streams"],
+                          "drained_paths": st["drained_paths"], "drain_launches": st["drain_launches"],
+                          "paths": st["paths"], **env,
+                          "env": {k: v for k, v in sorted(os.environ.items())
+                                  if k.startswith("SPT_") or k == "GPU_MAX_HW_QUEUES"}}), flush=True)
+        assert st["paths"] == paths and st["film_slots_unwritten"] == 0, st
 
 
 if __name__ == "__main__":
