@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0 = the CPUs this process may use: affinity mask and cgroup quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fused-leg", action="store_true",
+                    help="at N > 1, skip timing the fused pipeline beside the wavefront on the same tiles")
     ap.add_argument("--save", default="", help="write the rank-0 image (.npy) here")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
@@ -268,7 +270,6 @@ def main():
     dev = torch.device("cuda", local)
     tg = TileGather(H, W, rank, world, R, dev)
     film = tg.tile_view()
-    stream = torch.cuda.current_stream()
 
     def check_work(st):
         """Device-counted work of one render against the job (main.cpp:385-429
@@ -290,7 +291,10 @@ def main():
     # Consecutive steps alternate between two streams and two film buffers
     # (the library alternates two working sets), so a step's render can start
     # while the previous one drains; the gathers stay in step order.
-    streams = [stream, torch.cuda.Stream(device=dev)]
+    # two side streams, not the legacy default stream (whose implicit
+    # synchronisation semantics a caller overlapping work should avoid;
+    # DESIGN.md §6b)
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
     films = [film, tg.tile_view(1)]
     last_gather = [None]
 
@@ -351,7 +355,7 @@ def main():
         elapsed = time.perf_counter() - t0
         agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
                "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0,
-               "paths": 0}
+               "paths": 0, "drained_paths": 0, "drained_casts": 0, "drain_launches": 0, "drain_ms": 0.0}
         sts += [scene.render_wait(t) for t in tickets]
         for st in sts:
             check_work(st)
@@ -359,7 +363,9 @@ def main():
                 agg[k] += st[k]
         # consecutive renders overlap on the GPU (two streams, two working
         # sets): the kernel's busy time is the union of all their launch
-        # intervals on the scene's clock (spt_scene_isect_busy_end)
+        # intervals on the scene's clock (spt_scene_kernel_busy / _isect_busy_end)
+        agg["drain_busy_ms"], agg["drain_launches_timed"] = scene.kernel_busy(_lib.SPT_KERNEL_DRAIN)
+        agg["trace_busy_ms"], _ = scene.kernel_busy(_lib.SPT_KERNEL_ISECT | _lib.SPT_KERNEL_DRAIN)
         agg["isect_busy_ms"], nl = scene.isect_busy_end()
         if nl != agg["isect_launches"]:
             raise RuntimeError(f"isect intervals {nl} != timed launches {agg['isect_launches']}")
@@ -379,21 +385,21 @@ def main():
     if paths != W * H * args.spp * args.steps:
         raise RuntimeError(f"device-counted paths {paths} != {W * H * args.spp * args.steps} (W x H x spp x steps)")
     image_main = tg.image.clone() if rank == 0 else None
-    # At N > 1 the library's job-size rule runs the fused kernel on each rank's
-    # tile; the north-star wavefront pipeline is timed beside it on the same
-    # tiles (a second loop after the first), so the N-GPU line says what both do.
-    wave_leg = None
-    if world > 1 and st.get("fused") and args.pipeline == "auto":
+    # At N > 1 the fused pipeline is timed beside the wavefront on the same
+    # tiles (a second loop after the first), so the N-GPU line says how the
+    # north-star pipeline compares per tile (>= 0.9x).
+    other_leg = None
+    if world > 1 and args.pipeline == "auto" and not args.no_fused_leg:
+        other = "wavefront" if st.get("fused") else "fused"
         pw = sptamd.make_params(W, H, args.spp, args.depth, tile_index=rank, tile_count=world, rows_per_group=R,
-                                wavefront_paths=args.wavefront, timing=True, pipeline="wavefront", **kw)
+                                wavefront_paths=args.wavefront, timing=True, pipeline=other, **kw)
         w_el, w_agg, w_st, w_tot, w_gather_ms = timed_loop(pw)
         w_paths = w_tot[2]
-        wave_leg = {"pipeline": "wavefront", "value": round(w_paths / w_el / 1e6, 3),
-                    "ms_per_step": round(w_el / args.steps * 1e3, 3), "streams": w_st.get("streams"),
-                    "isect_busy_ms_per_step_rank0": round(w_agg["isect_busy_ms"] / args.steps, 4),
-                    "paths_device_counted": int(w_paths), "gather_ms": round(w_gather_ms, 4)}
+        other_leg = {"pipeline": other, "value": round(w_paths / w_el / 1e6, 3),
+                     "ms_per_step": round(w_el / args.steps * 1e3, 3), "streams": w_st.get("streams"),
+                     "paths_device_counted": int(w_paths), "gather_ms": round(w_gather_ms, 4)}
         if rank == 0 and image_main is not None:
-            wave_leg["image_equal_to_fused"] = bool(torch.equal(image_main, tg.image))
+            other_leg["image_equal"] = bool(torch.equal(image_main, tg.image))
     value = paths / elapsed / 1e6
     if rank == 0:
         # Roofline of the dominant kernel.  Wavefront:
@@ -416,52 +422,85 @@ def main():
         queue_cache = {0: None, 1: "cached", 2: "stream"}.get(st.get("queue_cache"), "?")
         if queue_cache and scene.backend.config["queue_cache"] == 0:
             queue_cache += " (auto)"
-        launches = max(agg["isect_launches"], 1)
-        avg_ms = agg["isect_ms"] / launches
-        casts_per_launch = agg["ray_casts"] / launches
+        # The wavefront's two tracing kernels: isect_queue_kernel (the casts
+        # of the per-cast launches, SURVEY §8(d)'s 52 B per cast) and the drain
+        # (render_fused_kernel's lane loop over a queue: it reads each queued
+        # path once and writes its film slot; the casts after that stay in
+        # registers).  The roofline names the one with the longer busy time
+        # (the union of its launch intervals over the timed renders).
+        isect_launches = max(agg["isect_launches"], 1)
         s_bar = agg_casts_all / paths
         c_bar = agg_cont_all / paths
         b_path = 84.0 + 120.0 * s_bar + 60.0 * c_bar
         unit_mode = not args.smallpt  # albedo 1, no emitters: the reference's case (one escape byte per path)
+        film_b = FUSED_BYTES_PER_PATH[unit_mode]
+        queue_b = 32 if unit_mode else 56  # PathQueue planes a queued path carries (q1, q2 [, q0, rad])
+        isect_casts = agg["ray_casts"] - agg["drained_casts"]
+        kernels = {}
         if fused:
-            bytes_per_unit = kernel_bytes_per_unit = FUSED_BYTES_PER_PATH[unit_mode]
-            total_bytes = agg["paths"] * bytes_per_unit  # rank 0's paths over rank 0's busy time
+            kernels["render_fused_kernel"] = dict(
+                units=agg["paths"], unit="path", bytes_per_unit=film_b, kernel_bytes_per_unit=film_b,
+                bytes=agg["paths"] * film_b, busy_ms=agg["isect_busy_ms"], launches=isect_launches,
+                sum_ms=agg["isect_ms"], casts=agg["ray_casts"],
+                basis="film bytes the fused kernel writes for rank 0's paths / union of its launch intervals")
         else:
-            bytes_per_unit, kernel_bytes_per_unit = ISECT_BYTES_PER_CAST, KERNEL_BYTES_PER_CAST
-            total_bytes = agg["ray_casts"] * ISECT_BYTES_PER_CAST
+            kernels["isect_queue_kernel"] = dict(
+                units=isect_casts, unit="ray cast", bytes_per_unit=ISECT_BYTES_PER_CAST,
+                kernel_bytes_per_unit=KERNEL_BYTES_PER_CAST, bytes=isect_casts * ISECT_BYTES_PER_CAST,
+                busy_ms=agg["isect_busy_ms"], launches=isect_launches, sum_ms=agg["isect_ms"], casts=isect_casts,
+                basis="algorithmic bytes of all isect launches / union of their intervals (isect busy)")
+            if agg["drain_launches"]:
+                kernels["render_fused_kernel<drain>"] = dict(
+                    units=agg["drained_paths"], unit="drained path", bytes_per_unit=queue_b + film_b,
+                    kernel_bytes_per_unit=queue_b + film_b, bytes=agg["drained_paths"] * (queue_b + film_b),
+                    busy_ms=agg["drain_busy_ms"], launches=max(agg["drain_launches_timed"], 1),
+                    sum_ms=agg["drain_ms"], casts=agg["drained_casts"],
+                    basis="queued path read once + its film write, per drained path / union of the drain "
+                          "launch intervals (the path's later casts stay in registers)")
+        dom_name = max(kernels, key=lambda k: kernels[k]["busy_ms"])
+        dom = kernels[dom_name]
+        launches = dom["launches"]
+        avg_ms = dom["sum_ms"] / launches
+        busy_ms = dom["busy_ms"]
+        bytes_per_unit, kernel_bytes_per_unit = dom["bytes_per_unit"], dom["kernel_bytes_per_unit"]
+        total_bytes = dom["bytes"]
         bytes_per_launch = total_bytes / launches
-        busy_ms = agg["isect_busy_ms"]
         achieved = total_bytes / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+        per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        kernel_table = {
+            k: {"busy_ms_per_step": round(v["busy_ms"] / args.steps, 4), "launches_per_step": round(v["launches"] / args.steps, 2),
+                "casts_per_step": round(v["casts"] / args.steps), "unit": v["unit"], "bytes_per_unit": v["bytes_per_unit"],
+                "achieved_gbs": round(v["bytes"] / (v["busy_ms"] * 1e-3) / 1e9, 2) if v["busy_ms"] > 0 else None,
+                "grays_per_s": round(v["casts"] / (v["busy_ms"] * 1e-3) / 1e9, 4) if v["busy_ms"] > 0 else None}
+            for k, v in kernels.items()}
         equiv = None
-        if fused:
-            eq_gbs = agg["paths"] * b_path / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
+        if dom["unit"] != "ray cast":
+            eq_gbs = paths / world * b_path / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
             equiv = {"bytes_per_path": round(b_path, 1), "achieved": round(eq_gbs, 2),
                      "frac": round(eq_gbs / HBM_PEAK_GBS, 5),
-                     "note": "SURVEY 8(d) whole-path bytes the wavefront would move for these paths, over the fused "
-                             "kernel's busy time; the fused kernel keeps them in registers"}
-        per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+                     "note": "SURVEY 8(d) whole-path bytes the per-cast launches would move for these paths, over the "
+                             "kernel's busy time; the lane loop keeps them in registers"}
         # whole-path bytes over the whole frame time, against the
         # spec peak and a stream-copy peak measured here (BASELINE.md plan)
         path_gbs = b_path * paths / elapsed / 1e9
         copy_gbs = stream_copy_gbs(torch, dev)
         build_id = _lib.lib.spt_build_id().decode()
         pmc = pmc_note = None
-        key = f"config{args.config}" + ("_fused" if fused else "")
+        key = f"config{args.config}" + ("_fused" if fused else "_drain" if dom_name.endswith("<drain>") else "")
         if os.path.exists(PMC_JSON) and world == 1:  # PMC passes (profiles/, tools/pmc_isect.sh)
             pmc = json.load(open(PMC_JSON)).get(key)
             if pmc and pmc.get("build_id") != build_id:
                 pmc_note = (f"{key} was measured on build {pmc.get('build_id')}, this library is {build_id}: "
                             "not used")
                 pmc = None
-        unit_name = "path" if fused else "cast"
+        unit_name = "cast" if dom["unit"] == "ray cast" else "path"
         traffic = traffic_per_unit = None
         if pmc and pmc.get(f"traffic_bytes_per_{unit_name}"):
             traffic_per_unit = pmc[f"traffic_bytes_per_{unit_name}"]
-            traffic = round(traffic_per_unit * (agg["paths"] / launches if fused else casts_per_launch))
+            traffic = round(traffic_per_unit * dom["units"] / launches)
         valu = None
         if pmc and pmc.get(f"valu_insts_per_{unit_name}") and busy_ms > 0:
-            units = agg["paths"] if fused else agg["ray_casts"]
-            rate = pmc[f"valu_insts_per_{unit_name}"] * units / (busy_ms * 1e-3) / 1e9
+            rate = pmc[f"valu_insts_per_{unit_name}"] * dom["units"] / (busy_ms * 1e-3) / 1e9
             valu = {f"insts_per_{unit_name}": round(pmc[f"valu_insts_per_{unit_name}"], 2), "achieved": round(rate, 1),
                     "peak": VALU_PEAK_G, "unit": "G wave64 VALU instr/s over kernel busy time",
                     "frac": round(rate / VALU_PEAK_G, 4)}
@@ -489,13 +528,20 @@ def main():
                                "else sample-major (DESIGN.md §4)",
             "queue_cache_rule": "auto: non-temporal path-queue / hit accesses for scenes of >= 256 MiB, else "
                                 "cached (DESIGN.md §4)",
-            "pipeline_rule": "auto: fused for tiles of <= 32M paths, else wavefront (DESIGN.md §6)"
+            "pipeline_rule": "auto: the wavefront (isect + ballot-compaction shade per cast; a job of <= 2^27 "
+                             "paths starts every path at once on one sub-wavefront and the drain finishes the "
+                             "paths still in flight after drain_casts casts; DESIGN.md §4, §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
-                       "hw_queues": {"requested": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                       "drain": None if fused else {
+                           "drained_paths_per_step": round(agg["drained_paths"] / args.steps),
+                           "drained_casts_per_step": round(agg["drained_casts"] / args.steps),
+                           "wavefront_casts_per_step": round((agg["ray_casts"] - agg["drained_casts"]) / args.steps),
+                           "drain_launches_per_step": round(agg["drain_launches"] / args.steps, 2)},
+                       "hw_queues": {"in_effect": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
                                      "environment": HW_QUEUES_ENV,
-                                     "note": "GPU_MAX_HW_QUEUES set by bench.py for its own process (SPT_HW_QUEUES "
-                                             "overrides); the library sets none (DESIGN.md §6b)"},
+                                     "note": "the environment's GPU_MAX_HW_QUEUES (SPT_HW_QUEUES overrides it for "
+                                             "an experiment); the library sets none (DESIGN.md §6b)"},
                        "workload": f"{args.scene} {W}x{H} {args.spp}spp depth {args.depth}"
                                    + (" (smallpt materials: Kd albedo, Ke light, black sky, RR from cast 5)"
                                       if args.smallpt else ""),
@@ -504,12 +550,13 @@ def main():
                        "work_order": work_order, "queue_cache": queue_cache},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                         "kernel": "render_fused_kernel" if fused else "isect_queue_kernel",
-                         "basis": ("film bytes the fused kernel writes for rank 0's paths / union of its fused "
-                                   "launch intervals") if fused else
-                                  "algorithmic bytes of all launches / union of their intervals (isect busy)",
+                         "kernel": dom_name,
+                         "basis": dom["basis"],
+                         "limiter": None if dom["unit"] == "ray cast" else
+                                    "latency of dependent node / triangle gathers and VALU issue (the lane loop keeps "
+                                    "a path in registers: its HBM bytes are the queue read and the film write)",
                          "bytes_per_unit": bytes_per_unit, "kernel_bytes_per_unit": kernel_bytes_per_unit,
-                         "unit_of_work": "path" if fused else "ray cast",
+                         "unit_of_work": dom["unit"],
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
                          "traffic_per_unit": traffic_per_unit,
                          "traffic_ratio": round(traffic / bytes_per_launch, 3) if traffic else None,
@@ -518,9 +565,12 @@ def main():
                                       "which overlap on two streams",
                          "launches_per_step": round(launches / args.steps, 2),
                          "avg_launch_ms": round(avg_ms, 4),
-                         "grays_per_s": round(agg["ray_casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None,
+                         "grays_per_s": round(dom["casts"] / (busy_ms * 1e-3) / 1e9, 4) if busy_ms else None,
                          "per_launch": {"achieved": round(per_launch, 2), "frac": round(per_launch / HBM_PEAK_GBS, 5),
-                                        "note": f"per-launch duration; {st.get('streams')} streams overlap"},
+                                        "note": f"per-launch duration; {st.get('streams')} stream(s) per render, "
+                                                "two renders overlap"},
+                         "kernels": kernel_table,
+                         "trace_busy_ms_per_step": round(agg["trace_busy_ms"] / args.steps, 4),
                          "pmc_source": os.path.relpath(PMC_JSON, ROOT) + "#" + key if pmc else None,
                          "pmc_note": pmc_note,
                          "build_id": build_id,
@@ -538,8 +588,8 @@ def main():
             "bvh": dict({k: sstats[k] for k in ("builder", "nodes", "max_depth", "build_ms", "sah_cost", "device_bytes")},
                         commit_s=round(t_commit, 3)),
         }
-        if wave_leg:
-            rec["wavefront_leg"] = wave_leg
+        if other_leg:
+            rec[other_leg["pipeline"] + "_leg"] = other_leg
         if args.save:
             np.save(args.save, image_main.cpu().numpy())
         if not args.no_cpu_baseline:

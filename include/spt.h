@@ -143,6 +143,8 @@ typedef struct spt_render_stats {
                                             back may overlap, and their union is the kernel's busy time */
     uint64_t drained_paths;     /* wavefront: paths the drain launches finished (spt_config.drain_q8) */
     uint64_t drain_launches;    /* wavefront: drain launches queued (each runs only if its queue is short) */
+    uint64_t drained_casts;     /* wavefront: ray casts the drain launches traced (the rest: isect launches) */
+    double drain_ms, drain_busy_ms; /* SPT_FLAG_TIMING: drain launch time summed / the union of its intervals */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -206,7 +208,7 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
  * SPT_ERR_INVALID for a value outside them.  Build fields are read only by
  * spt_scene_create_cfg; render / intersect fields by every later call. */
 enum {
-    SPT_PIPELINE_AUTO = 0,      /* fused iff W*H*spp of the tile <= fused_max_paths */
+    SPT_PIPELINE_AUTO = 0,      /* fused iff W*H*spp of the tile <= fused_max_paths (default 0: never) */
     SPT_PIPELINE_WAVEFRONT = 1, /* isect / shade / refill over path queues */
     SPT_PIPELINE_FUSED = 2      /* one persistent trace+shade kernel per sample chunk */
 };
@@ -231,7 +233,9 @@ typedef struct spt_config {
     uint32_t stack_slack;           /* extra LDS stack entries per lane (0)                  [0..64] */
     /* --- spt_render */
     uint32_t pipeline;              /* SPT_PIPELINE_* (the params' FUSED / WAVEFRONT flags win) [0..2] */
-    uint64_t fused_max_paths;       /* AUTO rule: fused for tiles of <= this many paths, 2^25       */
+    uint64_t fused_max_paths;       /* AUTO rule: fused for tiles of <= this many paths, 0 (the
+                                       wavefront with its drain matches or beats the fused kernel
+                                       at every tile size measured: DESIGN.md §6)              */
     uint32_t wavefront_paths;       /* paths in flight when params.wavefront_paths == 0, 2^25 [1..2^31) */
     uint32_t streams;               /* sub-wavefronts (HIP streams) of the wavefront, 4      [1..4] */
     uint32_t isect_refill_idle;     /* refill a wave once this many lanes are idle, 24       [1..64] */
@@ -285,6 +289,13 @@ typedef struct spt_config {
                                        length, this many casts after the stream's last work
                                        item started, and ends the stream's launches; 0: only
                                        on a short queue                                  [0..64] */
+    uint32_t fit_streams;           /* sub-wavefronts of a job that fits in flight (below), 1 [1..4] */
+    uint64_t fit_paths;             /* a job of at most this many paths (tile px x spp) starts every
+                                       path in the first refill (paths in flight = the job, unless
+                                       params.wavefront_paths is set) on fit_streams
+                                       sub-wavefronts: its last work item starts at once, so the
+                                       drain takes over drain_casts casts later; 2^27 (about 11 GB
+                                       of queues at most), 0: off               */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);
@@ -447,6 +458,13 @@ spt_status spt_render_wait(spt_scene scene, uint64_t ticket, spt_render_stats* s
  * union of all of them in ms and the number of launches, and stops collecting. */
 spt_status spt_scene_isect_busy_begin(spt_scene scene);
 spt_status spt_scene_isect_busy_end(spt_scene scene, double* busy_ms, uint64_t* launches);
+/* Between busy_begin and busy_end: the union of the launch intervals of the
+ * renders collected so far, for a mask of kernels (SPT_KERNEL_ISECT: the isect
+ * launches — the fused kernel's in the fused pipeline —, SPT_KERNEL_DRAIN: the
+ * wavefront's drain launches; both: the time either traced rays), and the
+ * number of launches.  Does not stop the collection. */
+enum { SPT_KERNEL_ISECT = 1u, SPT_KERNEL_DRAIN = 2u };
+spt_status spt_scene_kernel_busy(spt_scene scene, uint32_t kernels, double* busy_ms, uint64_t* launches);
 
 /* Rows of tile `tile_index` (in increasing order).  Returns the row count;
  * writes at most `cap` row indices into rows (may be NULL). */

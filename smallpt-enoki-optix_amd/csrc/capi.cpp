@@ -104,6 +104,7 @@ struct Stats {
                                   // wave steps running the triangle block, the visit block
     unsigned long long unwritten; // film slots still holding the sentinel at resolve time
     unsigned long long drained;   // paths finished by drain launches
+    unsigned long long drained_casts;  // ray casts traced by drain launches
 };
 
 constexpr int kMaxStreams = 4;
@@ -248,11 +249,12 @@ struct Workspace {
     RenderSlot slots[kRenderSlots];     // renders queued by spt_render_async (ticket % kRenderSlots)
     uint64_t next_ticket = 1;
     hipEvent_t epoch = nullptr;         // the first timed render's time origin: isect_begin/end_ms count from it
-    // spt_scene_isect_busy_begin/end: every isect launch interval (scene clock)
-    // of the renders collected in between, so the union across overlapping
-    // queued renders is exact (not one render's span less its overlap)
+    // spt_scene_isect_busy_begin/end: every isect [0] and drain [1] launch
+    // interval (scene clock) of the renders collected in between, so the union
+    // across overlapping queued renders is exact (not one render's span less
+    // its overlap)
     bool collect_iv = false;
-    std::vector<std::pair<double, double>> iv_all;
+    std::vector<std::pair<double, double>> iv_all[2];
 
     void release() {
         for (WorkSet& w : sets) w.release();
@@ -264,7 +266,7 @@ struct Workspace {
             for (auto e : r.events) (void)hipEventDestroy(e);
             if (r.done) (void)hipEventDestroy(r.done);
         }
-        iv_all.clear();
+        for (auto& v : iv_all) v.clear();
         collect_iv = false;
         const uint64_t t = next_ticket;  // tickets stay unique over the scene's life
         *this = Workspace();
@@ -530,6 +532,23 @@ spt_status render_slot(Workspace& ws, RenderSlot** out) {
     return SPT_OK;
 }
 
+// Total length of a set of intervals (their union), sorted by start.
+template <typename T>
+double interval_union(const std::vector<std::pair<T, T>>& iv) {
+    double busy = 0.0, lo = 0.0, hi = -1.0;
+    for (auto& x : iv) {
+        if (x.first > hi) {
+            if (hi > lo) busy += hi - lo;
+            lo = x.first;
+            hi = x.second;
+        } else {
+            hi = std::max<double>(hi, x.second);
+        }
+    }
+    if (hi > lo) busy += hi - lo;
+    return busy;
+}
+
 // Waits for a queued render and fills its statistics (device counters, the
 // union of its isect launch intervals, host wall time since it was queued).
 spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
@@ -539,7 +558,7 @@ spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
     if (rs.tile_rows) {  // an empty tile queued nothing
         HIP_TRY(hipEventSynchronize(r.done));
         const unsigned long long* hstats = reinterpret_cast<const unsigned long long*>(r.host);
-        static_assert(sizeof(Stats) == 12 * sizeof(unsigned long long), "Stats is the 12 counters read back here");
+        static_assert(sizeof(Stats) == 13 * sizeof(unsigned long long), "Stats is the 13 counters read back here");
         rs.ray_casts = hstats[0];
         rs.continuations = hstats[1];
         rs.regenerations = hstats[2] > r.regen_base ? hstats[2] - r.regen_base : 0;
@@ -555,46 +574,46 @@ spt_status render_collect(RenderSlot& r, Workspace& ws, spt_render_stats* out) {
         rs.isect_tri_wave_steps = hstats[8];
         rs.isect_node_wave_steps = hstats[9];
         rs.drained_paths = hstats[11];
+        rs.drained_casts = hstats[12];
         if (r.timing) {
             uint64_t nis = 0;
-            std::vector<std::pair<float, float>> iv;  // isect launch intervals from the origin
+            // launch intervals from the origin: [0] isect (the fused kernel in
+            // the fused pipeline), [1] the wavefront's drain
+            std::vector<std::pair<float, float>> iv[2];
             for (auto& tk : r.timed) {
                 float ms = 0.0f;
                 HIP_TRY(hipEventElapsedTime(&ms, r.events[tk.first], r.events[tk.first + 1]));
                 if (tk.second == 0) rs.camera_ms += ms;
-                else if (tk.second == 1) {
-                    rs.isect_ms += ms;
-                    nis++;
+                else if (tk.second == 1 || tk.second == 4) {
                     float t0 = 0.0f;
                     HIP_TRY(hipEventElapsedTime(&t0, r.events[0], r.events[tk.first]));
-                    iv.push_back({t0, t0 + ms});
+                    if (tk.second == 1) {
+                        rs.isect_ms += ms;
+                        nis++;
+                    } else {
+                        rs.drain_ms += ms;
+                    }
+                    iv[tk.second == 4].push_back({t0, t0 + ms});
                 } else if (tk.second == 2) rs.shade_ms += ms;
                 else rs.resolve_ms += ms;
             }
             rs.isect_launches = nis;
             // launches on the K streams overlap: busy time = union of their intervals
-            std::sort(iv.begin(), iv.end());
-            if (!iv.empty() && epoch) {  // the span on the scene's clock, for unions across queued renders
+            for (auto& v : iv) std::sort(v.begin(), v.end());
+            if (!iv[0].empty() && epoch) {  // the span on the scene's clock, for unions across queued renders
                 float t_origin = 0.0f;
                 HIP_TRY(hipEventElapsedTime(&t_origin, epoch, r.events[0]));
-                float last = iv[0].second;
-                for (auto& x : iv) last = std::max(last, x.second);
-                rs.isect_begin_ms = (double)t_origin + iv[0].first;
+                float last = iv[0][0].second;
+                for (auto& x : iv[0]) last = std::max(last, x.second);
+                rs.isect_begin_ms = (double)t_origin + iv[0][0].first;
                 rs.isect_end_ms = (double)t_origin + last;
                 if (ws.collect_iv)
-                    for (auto& x : iv) ws.iv_all.push_back({(double)t_origin + x.first, (double)t_origin + x.second});
+                    for (int k = 0; k < 2; k++)
+                        for (auto& x : iv[k])
+                            ws.iv_all[k].push_back({(double)t_origin + x.first, (double)t_origin + x.second});
             }
-            float lo = 0.0f, hi = -1.0f;
-            for (auto& x : iv) {
-                if (x.first > hi) {
-                    if (hi > lo) rs.isect_busy_ms += hi - lo;
-                    lo = x.first;
-                    hi = x.second;
-                } else {
-                    hi = std::max(hi, x.second);
-                }
-            }
-            if (hi > lo) rs.isect_busy_ms += hi - lo;
+            rs.isect_busy_ms = interval_union(iv[0]);
+            rs.drain_busy_ms = interval_union(iv[1]);
         }
     }
     rs.total_ms = now_ms() - r.wall0;
@@ -650,6 +669,8 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(drain_q8, 0, 65535)
     CFG_RANGE(drain_grid_q8, 0, 4096)
     CFG_RANGE(drain_casts, 0, 64)
+    CFG_RANGE(fit_streams, 1, kMaxStreams)
+    CFG_RANGE(fit_paths, 0, 1ull << 31)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -1022,7 +1043,7 @@ void spt_default_config(spt_config* c) {
     c->ploc_radius = 16;
     c->stack_slack = 0;
     c->pipeline = SPT_PIPELINE_AUTO;
-    c->fused_max_paths = 1ull << 25;
+    c->fused_max_paths = 0;
     c->wavefront_paths = kDefaultWavefrontPaths;
     c->streams = 4;
     c->isect_refill_idle = 24;
@@ -1044,6 +1065,8 @@ void spt_default_config(spt_config* c) {
     c->drain_q8 = kDefaultDrainQ8;
     c->drain_grid_q8 = 0;
     c->drain_casts = kDefaultDrainCasts;
+    c->fit_streams = 1;
+    c->fit_paths = kDefaultFitPaths;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1845,6 +1868,16 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         (cfg.queue_cache == SPT_QUEUE_CACHE_AUTO && scene_bytes >= kPixelMajorMinSceneBytes);
     if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
         C = kPixelMajorWavefrontPaths;
+    // A job that fits in flight (spt_config.fit_paths): every path starts in
+    // the first refill on fit_streams sub-wavefronts, so its last work item
+    // starts at once and the drain finishes it drain_casts casts later.  The
+    // per-cast launches then run only while the whole job is in flight, and
+    // a render is a handful of launches, which two renders queued on two
+    // streams overlap without sub-wavefront streams of their own (DESIGN.md §6:
+    // stable at the box's four hardware queues, where four sub-wavefront
+    // streams per working set could share a queue with the other set's).
+    const bool fit = !fused && !p.wavefront_paths && cfg.fit_paths && cfg.drain_q8 && P * p.spp <= cfg.fit_paths;
+    if (fit) C = P * p.spp;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);
@@ -1852,7 +1885,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // sub-wavefront's launch tail overlaps the others' work.
     // Measured on the headline config: 1 stream 1982, 2: 2649, 3: 2769, 4: 2791 Mpaths/s
     // (4 = the box's hardware queues per process, GPU_MAX_HW_QUEUES).
-    int K = fused ? 1 : (int)cfg.streams;
+    int K = fused ? 1 : fit ? (int)cfg.fit_streams : (int)cfg.streams;
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
@@ -1946,7 +1979,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     auto mark = [&](int kind, hipStream_t sk, auto&& launch) -> spt_status {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         spt_status s2;
-        const bool tm = kind == 1 ? timing : timing_all;
+        const bool tm = (kind == 1 || kind == 4) ? timing : timing_all;  // isect and drain: the tracing kernels
         if (tm) {
             if ((s2 = get_event(*slot, ev, &e0)) || (s2 = get_event(*slot, ev + 1, &e1))) return s2;
             HIP_TRY(hipEventRecord(e0, sk));
@@ -2034,6 +2067,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             D.sflag = sflag;
             D.stats = slot->dev->stats;
             D.drained = &slot->dev->drained;
+            D.drained_casts = &slot->dev->drained_casts;
             D.next = &b.cnt->isect_next;  // zeroed by the refill before; an isect that skips leaves it
             D.initstate = p.rng_initstate;
             D.P = (uint32_t)P; D.W = p.width; D.max_depth = p.max_depth;
@@ -2205,7 +2239,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         da[k].q = q[k][c];
                         da[k].qcount = &b.cnt->qn[c];
                         da[k].drain_below = 0xffffffffu;
-                        if ((st = mark(1, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
+                        if ((st = mark(4, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
                         drain_launches++;
                         // the refill's bookkeeping: the drained paths' first casts
                         ra[k].q = q[k][nx]; ra[k].surv = &b.cnt->surv[nx]; ra[k].cursor_in = &b.cnt->cursor[c];
@@ -2234,7 +2268,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         da[k].q = q[k][c];
                         da[k].qcount = &b.cnt->qn[c];
                         da[k].drain_below = drain_T[k];
-                        if ((st = mark(1, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
+                        if ((st = mark(4, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
                         drain_launches++;
                     }
                     if (cam) {  // no refill launch: the next isect starts the new paths
@@ -2353,8 +2387,22 @@ spt_status spt_render(spt_scene sc, const spt_render_params* pp, float* film_dev
 spt_status spt_scene_isect_busy_begin(spt_scene sc) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_isect_busy_begin: NULL scene");
     std::lock_guard<std::mutex> lock(sc->mu);
-    sc->ws.iv_all.clear();
+    for (auto& v : sc->ws.iv_all) v.clear();
     sc->ws.collect_iv = true;
+    return SPT_OK;
+}
+
+spt_status spt_scene_kernel_busy(spt_scene sc, uint32_t kernels, double* busy_ms, uint64_t* launches) {
+    if (!sc || !busy_ms) return fail(SPT_ERR_INVALID, "spt_scene_kernel_busy: NULL argument");
+    if (kernels == 0 || kernels > (SPT_KERNEL_ISECT | SPT_KERNEL_DRAIN))
+        return fail(SPT_ERR_INVALID, "spt_scene_kernel_busy: kernels must be a non-empty mask of SPT_KERNEL_*");
+    std::lock_guard<std::mutex> lock(sc->mu);
+    std::vector<std::pair<double, double>> iv;
+    if (kernels & SPT_KERNEL_ISECT) iv.insert(iv.end(), sc->ws.iv_all[0].begin(), sc->ws.iv_all[0].end());
+    if (kernels & SPT_KERNEL_DRAIN) iv.insert(iv.end(), sc->ws.iv_all[1].begin(), sc->ws.iv_all[1].end());
+    std::sort(iv.begin(), iv.end());
+    *busy_ms = interval_union(iv);
+    if (launches) *launches = iv.size();
     return SPT_OK;
 }
 
@@ -2362,21 +2410,11 @@ spt_status spt_scene_isect_busy_end(spt_scene sc, double* busy_ms, uint64_t* lau
     if (!sc || !busy_ms) return fail(SPT_ERR_INVALID, "spt_scene_isect_busy_end: NULL argument");
     std::lock_guard<std::mutex> lock(sc->mu);
     std::vector<std::pair<double, double>> iv;
-    iv.swap(sc->ws.iv_all);
+    iv.swap(sc->ws.iv_all[0]);
+    sc->ws.iv_all[1].clear();
     sc->ws.collect_iv = false;
     std::sort(iv.begin(), iv.end());
-    double busy = 0.0, lo = 0.0, hi = -1.0;
-    for (auto& x : iv) {
-        if (x.first > hi) {
-            if (hi > lo) busy += hi - lo;
-            lo = x.first;
-            hi = x.second;
-        } else {
-            hi = std::max(hi, x.second);
-        }
-    }
-    if (hi > lo) busy += hi - lo;
-    *busy_ms = busy;
+    *busy_ms = interval_union(iv);
     if (launches) *launches = iv.size();
     return SPT_OK;
 }

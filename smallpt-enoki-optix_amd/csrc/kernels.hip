@@ -1470,8 +1470,13 @@ void render_fused_kernel(FusedArgs a) {
         }
     }
     // the drain: a queued path's first cast here was counted with the queue
-    // (by the refill that follows), so only the casts after it are added
+    // (by the refill that follows), so only the casts after it are added;
+    // every cast it traced goes to drained_casts
     if constexpr (kDrain) {
+        uint32_t dc = casts;
+#pragma unroll
+        for (uint32_t off = 32; off > 0; off >>= 1) dc += (uint32_t)__shfl_down((int)dc, off);
+        if ((threadIdx.x & 63u) == 0 && dc) atomicAdd(a.drained_casts, (unsigned long long)dc);
         casts = conts;
         starts = 0;
     }

@@ -52,10 +52,12 @@ constexpr uint32_t kDefaultWavefrontPaths = 1u << 25;
 constexpr uint64_t kPixelMajorWavefrontPaths = 24ull << 20;
 // spt_config.drain_q8 default: a sub-wavefront's queue shorter than this many
 // 1/256ths of its persistent isect lanes goes to the drain launch
-constexpr uint32_t kDefaultDrainQ8 = 512;
+constexpr uint32_t kDefaultDrainQ8 = 1024;
+// spt_config.fit_paths default: jobs of at most 2^27 paths start every path at once
+constexpr uint64_t kDefaultFitPaths = 1ull << 27;
 // spt_config.drain_casts default: the drain runs this many casts after a
 // sub-wavefront's last work item started, whatever its queue holds
-constexpr uint32_t kDefaultDrainCasts = 3;
+constexpr uint32_t kDefaultDrainCasts = 1;
 
 // Path modes: what a path carries besides its ray.  The scene decides
 // (spt_render): unit = every albedo 1 and no emitters, the reference's own
@@ -356,6 +358,7 @@ struct FusedArgs {
     uint32_t drain_below;
     uint32_t nt;                    // 1: non-temporal queue loads (spt_config.queue_cache)
     unsigned long long* drained;    // paths the drain launches took over
+    unsigned long long* drained_casts;  // ray casts the drain launches traced
 };
 
 struct HitInfoArgs {

@@ -35,12 +35,13 @@ EXPORTED = [
     "spt_default_config", "spt_scene_create_cfg", "spt_scene_set_config", "spt_scene_get_config",
     "spt_bvh_build_stats", "spt_scene_set_texture", "spt_scene_set_spheres", "spt_scene_set_material_kinds",
     "spt_scene_save", "spt_scene_load", "spt_scene_cache_info",
-    "spt_scene_isect_busy_begin", "spt_scene_isect_busy_end",
+    "spt_scene_isect_busy_begin", "spt_scene_isect_busy_end", "spt_scene_kernel_busy",
 ]
 SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
 SPT_WORK_AUTO, SPT_WORK_SAMPLE_MAJOR, SPT_WORK_PIXEL_MAJOR = 0, 1, 2
 SPT_QUEUE_CACHE_AUTO, SPT_QUEUE_CACHE_CACHED, SPT_QUEUE_CACHE_STREAM = 0, 1, 2
+SPT_KERNEL_ISECT, SPT_KERNEL_DRAIN = 1, 2
 
 
 class SptError(RuntimeError):
@@ -93,7 +94,8 @@ class RenderStats(ctypes.Structure):
                 ("work_order", c_uint32), ("queue_cache", c_uint32),
                 ("isect_tri_wave_steps", c_uint64), ("isect_node_wave_steps", c_uint64),
                 ("isect_begin_ms", c_double), ("isect_end_ms", c_double),
-                ("drained_paths", c_uint64), ("drain_launches", c_uint64)]
+                ("drained_paths", c_uint64), ("drain_launches", c_uint64), ("drained_casts", c_uint64),
+                ("drain_ms", c_double), ("drain_busy_ms", c_double)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -120,7 +122,8 @@ class Config(ctypes.Structure):
                 ("plane_pad", c_uint32), ("film_budget_bytes", c_uint64),
                 ("public_persistent", c_uint32), ("public_refill_idle", c_uint32), ("pack_groups", c_uint32),
                 ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32),
-                ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32)]
+                ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32),
+                ("fit_streams", c_uint32), ("fit_paths", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -166,6 +169,7 @@ def _load() -> ctypes.CDLL:
         "spt_render_wait": (i32, [vp, u64, POINTER(RenderStats)]),
         "spt_scene_isect_busy_begin": (i32, [vp]),
         "spt_scene_isect_busy_end": (i32, [vp, POINTER(ctypes.c_double), POINTER(u64)]),
+        "spt_scene_kernel_busy": (i32, [vp, u32, POINTER(ctypes.c_double), POINTER(u64)]),
         "spt_tile_rows": (u32, [u32, u32, u32, u32, vp, u32]),
         "spt_default_params": (None, [POINTER(RenderParams)]),
         "spt_last_error": (c_char_p, []),
@@ -246,6 +250,8 @@ _ENV_CONFIG = {
     "SPT_DRAIN_Q8": ("drain_q8", int),
     "SPT_DRAIN_GRID_Q8": ("drain_grid_q8", int),
     "SPT_DRAIN_CASTS": ("drain_casts", int),
+    "SPT_FIT_STREAMS": ("fit_streams", int),
+    "SPT_FIT_PATHS": ("fit_paths", int),
 }
 
 

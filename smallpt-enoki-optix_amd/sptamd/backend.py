@@ -413,6 +413,15 @@ class Scene:
         """spt_scene_isect_busy_begin: start collecting isect launch intervals."""
         check(lib.spt_scene_isect_busy_begin(self.backend.handle), "spt_scene_isect_busy_begin")
 
+    def kernel_busy(self, kernels: int = _lib.SPT_KERNEL_ISECT) -> Tuple[float, int]:
+        """spt_scene_kernel_busy: (union of the isect / drain launch intervals
+        collected since isect_busy_begin, in ms; launches), without stopping
+        the collection.  kernels: a mask of _lib.SPT_KERNEL_*."""
+        ms, n = ctypes.c_double(0.0), ctypes.c_uint64(0)
+        check(lib.spt_scene_kernel_busy(self.backend.handle, kernels, ctypes.byref(ms), ctypes.byref(n)),
+              "spt_scene_kernel_busy")
+        return ms.value, n.value
+
     def isect_busy_end(self) -> Tuple[float, int]:
         """spt_scene_isect_busy_end: (union of the intervals collected since
         isect_busy_begin in ms, launches) across every render collected."""

@@ -1,0 +1,100 @@
+"""The wavefront's drain (kernels.hip render_fused_kernel<kDrain>, capi.cpp
+spt_render_async): once a sub-wavefront's last work item has started, a queue
+shorter than drain_q8/256 of its isect lanes — or any queue drain_casts casts
+later — is finished by one launch whose lanes continue each path in registers.
+Every combination must give the oracle's bits and the device-counted work:
+threshold only, forced only, both; 1 and 3 sub-wavefronts; jobs that fit in
+flight (fit_paths) and jobs that refill (wavefront_paths set); the
+reference's unit mode, albedo + roulette, emitters + smallpt spheres with
+mirror / glass; sample chunks (film_budget_bytes)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import sptamd
+from conftest import assert_work_complete
+from sptamd import scenes
+
+pytestmark = pytest.mark.gpu
+W, H, SPP, D = 40, 32, 6, 6
+
+
+@pytest.fixture(scope="module")
+def mesh():
+    return scenes.mitsuba_synth(detail=0.25)
+
+
+def materials(mesh, mode):
+    nm = len(mesh["kd"])
+    rng = np.random.default_rng(4)
+    if mode == "unit":
+        return {}
+    alb = rng.uniform(0.3, 0.95, size=(nm, 3)).astype(np.float32)
+    if mode == "albedo":
+        return {"albedo": alb}
+    emi = np.zeros((nm, 3), np.float32)
+    emi[4] = (2.0, 1.5, 1.0)
+    kinds = np.zeros(nm, np.uint32)
+    kinds[2], kinds[3] = 1, 2  # mirror, glass
+    return {"albedo": alb, "emission": emi, "kinds": kinds,
+            "spheres": np.array([[0.0, 0.6, 0.0, 0.35], [0.7, 0.3, 0.4, 0.2]], np.float32),
+            "sphere_mat": np.array([2, 3], np.int32)}
+
+
+def gpu_scene(mesh, mat, **knobs):
+    cfg = sptamd.default_config()
+    for k, v in knobs.items():
+        setattr(cfg, k, v)
+    s = sptamd.Scene(config=cfg)
+    s.add_arrays(mesh)
+    s.commit(0)
+    if "albedo" in mat:
+        s.backend.set_albedo(mat["albedo"])
+    if "emission" in mat:
+        s.backend.set_emission(mat["emission"])
+    if "spheres" in mat:
+        s.backend.set_spheres(mat["spheres"], mat["sphere_mat"])
+        s.backend.set_material_kinds(mat["kinds"])
+    return s
+
+
+@pytest.mark.parametrize("mode", ["unit", "albedo", "emit_spheres"])
+@pytest.mark.parametrize("q8,casts", [(0, 0), (1, 0), (1024, 0), (65535, 0), (1024, 1), (0, 3), (1024, 2)])
+@pytest.mark.parametrize("streams,wf", [(1, 0), (3, 0), (1, 700), (3, 1500)])
+def test_drain_bitexact(mesh, mode, q8, casts, streams, wf, monkeypatch):
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, mode)
+    knobs = dict(drain_q8=q8, drain_casts=casts, streams=streams, fit_streams=streams)
+    s = gpu_scene(mesh, mat, **knobs)
+    kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
+    film, st = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, **kw))
+    torch.cuda.synchronize()
+    osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
+                        sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
+    ref, casts_ref = osc.render(O.reference_params(W, H, SPP, D, **kw))
+    np.testing.assert_array_equal(film.cpu().numpy(), ref)
+    assert st["ray_casts"] == casts_ref
+    assert_work_complete(st, H, W, SPP)
+    assert st["drained_casts"] <= st["ray_casts"] and st["drained_paths"] <= st["paths"]
+    if q8 == 0:
+        assert st["drained_paths"] == 0 and st["drain_launches"] == 0
+    if q8 == 65535:  # every short queue drains at once: nothing after the first drained cast
+        assert st["drained_paths"] > 0
+    if q8 and casts and not wf:  # the job fits: the drain runs `casts` casts after the start
+        assert st["drained_paths"] > 0 and st["streams"] == streams
+
+
+def test_drain_sample_chunks(mesh, monkeypatch):
+    """Several film chunks (film_budget_bytes): each chunk's queue drains."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, "albedo")
+    s = gpu_scene(mesh, mat, film_budget_bytes=12 * W * H * 2)
+    kw = dict(rr_start_depth=2)
+    film, st = s.render(sptamd.make_params(W, H, 7, D, **kw))
+    torch.cuda.synchronize()
+    ref, casts = O.OracleScene(mesh, albedo=mat["albedo"]).render(O.reference_params(W, H, 7, D, **kw))
+    np.testing.assert_array_equal(film.cpu().numpy(), ref)
+    assert st["ray_casts"] == casts and st["drained_paths"] > 0

@@ -53,10 +53,24 @@ def render(scene, w, h, spp, depth, **kw):
     return film.cpu().numpy(), st
 
 
-@pytest.mark.parametrize("pipeline", ["wavefront", "fused"])
-def test_config0_whole_image_bitexact(gscene, oscene, pipeline):
+PIPELINES = ["wavefront", "fused", "percast"]  # percast: the wavefront with no drain (spt_config.drain_q8 = 0)
+
+
+def pipeline_kw(pipeline, monkeypatch):
+    if pipeline == "percast":
+        monkeypatch.setenv("SPT_DRAIN_Q8", "0")
+        return "wavefront"
+    return pipeline
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_config0_whole_image_bitexact(gscene, oscene, pipeline, monkeypatch):
     """BASELINE configs[0]: 256 x 256, 4 spp, max depth 4 — every pixel."""
-    got, st = render(gscene, 256, 256, 4, 4, pipeline=pipeline)
+    got, st = render(gscene, 256, 256, 4, 4, pipeline=pipeline_kw(pipeline, monkeypatch))
+    if pipeline == "percast":
+        assert st["drained_paths"] == 0 and st["drain_launches"] == 0
+    elif pipeline == "wavefront":
+        assert 0 < st["drained_paths"] < st["paths"] and 0 < st["drained_casts"] < st["ray_casts"]
     ref, casts = oscene.render(O.reference_params(256, 256, 4, 4), nthreads=THREADS)
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts and st["paths"] == 256 * 256 * 4
@@ -67,12 +81,12 @@ def test_config0_whole_image_bitexact(gscene, oscene, pipeline):
     assert_within_tolerance(got, alt, 4, "gpu vs oracle(all variants)")
 
 
-@pytest.mark.parametrize("pipeline", ["wavefront", "fused"])
-def test_reference_default_whole_image_bitexact(gscene, oscene, pipeline):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_reference_default_whole_image_bitexact(gscene, oscene, pipeline, monkeypatch):
     """The reference's hard-coded run, main.cpp:357-361: 512^2 x 100 spp x 2 casts."""
     p = sptamd.default_params()
     assert (p.width, p.height, p.spp, p.max_depth) == (512, 512, 100, 2)
-    got, st = render(gscene, 512, 512, 100, 2, pipeline=pipeline)
+    got, st = render(gscene, 512, 512, 100, 2, pipeline=pipeline_kw(pipeline, monkeypatch))
     ref, casts = oscene.render(O.reference_params(512, 512, 100, 2), nthreads=THREADS)
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts

@@ -160,7 +160,11 @@ def test_config_defaults_and_env_overrides():
     c = sptamd.default_config()
     assert (c.build, c.bvh_width, c.collapse, c.ploc_radius) == (0, 6, 0, 16)
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
-    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 25      # spt.h docs = code
+    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 0            # spt.h docs = code
+    assert (c.drain_q8, c.drain_grid_q8, c.drain_casts) == (1024, 0, 1)
+    assert (c.fit_streams, c.fit_paths) == (1, 1 << 27)
+    d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
+    assert (d.drain_q8, d.drain_casts, d.fit_paths) == (0, 4, 0)
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
     assert c.pack_groups == 1
     assert (c.work_order, c.queue_cache) == (_lib.SPT_WORK_AUTO, _lib.SPT_QUEUE_CACHE_AUTO)
@@ -175,7 +179,9 @@ def test_config_defaults_and_env_overrides():
 @pytest.mark.parametrize("field,value", [("streams", 0), ("streams", 5), ("bvh_width", 4), ("ploc_radius", 12),
                                          ("isect_refill_idle", 65), ("film_budget_bytes", 0), ("pipeline", 3),
                                          ("bvh_width", 7), ("pack_groups", 3), ("work_order", 3),
-                                         ("queue_cache", 3)])
+                                         ("queue_cache", 3), ("drain_q8", 65536), ("drain_grid_q8", 4097),
+                                         ("drain_casts", 65), ("fit_streams", 0), ("fit_streams", 5),
+                                         ("fit_paths", (1 << 31) + 1)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)

@@ -36,6 +36,7 @@ for s in "$@"; do
     bench1gq) run bench1gq 600 env SPT_BUILD=gpu python bench.py --config 1 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench1x3) for r in 1 2 3; do run bench1_$r 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline; done ;;
     bench10) run bench10 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     bench1f) run bench1f 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --pipeline fused ;;
     bench0|bench2|bench3|bench4) run $s 600 python bench.py --config ${s#bench} --steps 2 --warmup 1 ;;

@@ -70,7 +70,10 @@ def run_tiles(args, scene, cfg, kw, W, H, spp, D, env):
                                wavefront_paths=args.wavefront, **kw)
         rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
         films = [torch.empty((3, rows, W), dtype=torch.float32, device="cuda") for _ in range(2)]
-        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        # the two caller streams renders alternate on (bench.py: the current
+        # stream and one more); SPT_SIM_POOL=1: two pool streams, no null stream
+        streams = ([torch.cuda.Stream(), torch.cuda.Stream()] if os.environ.get("SPT_SIM_POOL") == "1"
+                   else [torch.cuda.current_stream(), torch.cuda.Stream()])
         for k in range(2):  # one setup render per stream (working set) before the timed steps, as bench.py
             scene.render_wait(scene.render_async(p, film=films[k], stream=streams[k])[1])
         torch.cuda.synchronize()
