@@ -17,6 +17,7 @@ host, and the parity of the (assembled) image against that oracle render.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -36,6 +37,7 @@ HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
 if os.environ.get("SPT_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ["SPT_HW_QUEUES"]
 
+PG_TIMEOUT = datetime.timedelta(minutes=20)  # torch.distributed collectives (CPU baseline on rank 0)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_JSON = os.path.join(ROOT, "profiles", "isect_pmc.json")  # tools/pmc_isect.sh output
 VALU_PEAK_G = 256 * 4 * 2.4 / 2  # wave64 VALU instr/s (G): 1024 SIMDs, 2 cycles each at 2.4 GHz (MI355X_MICROARCH.md)
@@ -230,9 +232,11 @@ def main():
     if world > 1:
         backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # rank 0 times the CPU baseline (up to ~40 s on config 4) while the
+            # others wait at a barrier: a timeout well past that
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=PG_TIMEOUT)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=PG_TIMEOUT)
 
     # scene: generated stand-in, loaded through the OBJ reader like main.cpp:365
     # (rank 0 writes the cached OBJ first)
@@ -469,7 +473,8 @@ def main():
         per_launch = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         kernel_table = {
             k: {"busy_ms_per_step": round(v["busy_ms"] / args.steps, 4), "launches_per_step": round(v["launches"] / args.steps, 2),
-                "casts_per_step": round(v["casts"] / args.steps), "unit": v["unit"], "bytes_per_unit": v["bytes_per_unit"],
+                "casts_per_step": round(v["casts"] / args.steps), "units_per_step": round(v["units"] / args.steps),
+                "unit": v["unit"], "bytes_per_unit": v["bytes_per_unit"],
                 "achieved_gbs": round(v["bytes"] / (v["busy_ms"] * 1e-3) / 1e9, 2) if v["busy_ms"] > 0 else None,
                 "grays_per_s": round(v["casts"] / (v["busy_ms"] * 1e-3) / 1e9, 4) if v["busy_ms"] > 0 else None}
             for k, v in kernels.items()}
@@ -493,15 +498,16 @@ def main():
                 pmc_note = (f"{key} was measured on build {pmc.get('build_id')}, this library is {build_id}: "
                             "not used")
                 pmc = None
-        unit_name = "cast" if dom["unit"] == "ray cast" else "path"
+        # PMC figures are per ray cast for every kernel (the drain and the
+        # fused kernel also per path), so the same basis serves any of them
         traffic = traffic_per_unit = None
-        if pmc and pmc.get(f"traffic_bytes_per_{unit_name}"):
-            traffic_per_unit = pmc[f"traffic_bytes_per_{unit_name}"]
-            traffic = round(traffic_per_unit * dom["units"] / launches)
+        if pmc and pmc.get("traffic_bytes_per_cast"):
+            traffic_per_unit = pmc["traffic_bytes_per_cast"]
+            traffic = round(traffic_per_unit * dom["casts"] / launches)
         valu = None
-        if pmc and pmc.get(f"valu_insts_per_{unit_name}") and busy_ms > 0:
-            rate = pmc[f"valu_insts_per_{unit_name}"] * dom["units"] / (busy_ms * 1e-3) / 1e9
-            valu = {f"insts_per_{unit_name}": round(pmc[f"valu_insts_per_{unit_name}"], 2), "achieved": round(rate, 1),
+        if pmc and pmc.get("valu_insts_per_cast") and busy_ms > 0:
+            rate = pmc["valu_insts_per_cast"] * dom["casts"] / (busy_ms * 1e-3) / 1e9
+            valu = {"insts_per_cast": round(pmc["valu_insts_per_cast"], 2), "achieved": round(rate, 1),
                     "peak": VALU_PEAK_G, "unit": "G wave64 VALU instr/s over kernel busy time",
                     "frac": round(rate / VALU_PEAK_G, 4)}
         rec = {
@@ -558,8 +564,11 @@ def main():
                          "bytes_per_unit": bytes_per_unit, "kernel_bytes_per_unit": kernel_bytes_per_unit,
                          "unit_of_work": dom["unit"],
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
-                         "traffic_per_unit": traffic_per_unit,
+                         "traffic_per_cast": traffic_per_unit,
                          "traffic_ratio": round(traffic / bytes_per_launch, 3) if traffic else None,
+                         "traffic_note": "HBM-side bytes per launch from the PMC passes (2 x FETCH_SIZE + WRITE_SIZE, "
+                                         "MI355X_MICROARCH.md gfx950 correction) of this build: node and triangle "
+                                         "gathers the caches miss, besides the algorithmic bytes",
                          "busy_ms_per_step": round(busy_ms / args.steps, 4),
                          "busy_note": "union over the step's launch intervals and over consecutive steps' renders, "
                                       "which overlap on two streams",

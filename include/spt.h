@@ -289,13 +289,20 @@ typedef struct spt_config {
                                        length, this many casts after the stream's last work
                                        item started, and ends the stream's launches; 0: only
                                        on a short queue                                  [0..64] */
-    uint32_t fit_streams;           /* sub-wavefronts of a job that fits in flight (below), 1 [1..4] */
+    uint32_t fit_streams;           /* sub-wavefronts of a job that fits in flight (below), 2; 1 on
+                                       a caller's null stream (shared hardware queues)        [1..4] */
     uint64_t fit_paths;             /* a job of at most this many paths (tile px x spp) starts every
                                        path in the first refill (paths in flight = the job, unless
                                        params.wavefront_paths is set) on fit_streams
                                        sub-wavefronts: its last work item starts at once, so the
                                        drain takes over drain_casts casts later; 2^27 (about 11 GB
                                        of queues at most), 0: off               */
+    uint32_t sub_queues;            /* 1: a render runs on its working set's own streams, created
+                                       with a full CU mask, which gives each a hardware queue of
+                                       its own whatever GPU_MAX_HW_QUEUES allows; they are blocking
+                                       streams, so a set bound to the legacy null stream uses plain
+                                       non-blocking streams instead.  0: plain streams always
+                                       (they share the process's queues)       [0..1] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -141,7 +141,8 @@ struct Sub {
     char* qb = nullptr;
     char* hits = nullptr;
     Counters* cnt = nullptr;
-    hipStream_t stream = nullptr;       // internal stream (sub 0 runs on the caller's)
+    hipStream_t stream = nullptr;       // the library's own stream (spt_config.sub_queues)
+    bool own_queue = false;             // created with a full CU mask (spt_config.sub_queues)
     Counters* host_cnt = nullptr;       // pinned, 2 slots (counter snapshots read one batch behind)
     hipEvent_t count_ev[2] = {nullptr, nullptr};
     hipEvent_t join_ev = nullptr;
@@ -162,7 +163,8 @@ struct WorkSet {
     char* film = nullptr;               // per-sample contributions of a chunk (bytes or RGB floats)
     float* acc = nullptr;               // [3][P] running sum across chunks
     hipEvent_t fork_ev = nullptr;
-    hipEvent_t free_ev = nullptr;       // recorded on the stream of the last render that used the set
+    hipEvent_t free_ev = nullptr;       // recorded on the set's stream 0 after the last render that used it
+    hipEvent_t call_ev = nullptr;       // the caller stream's work before a render (the render waits for it)
     bool used = false;                  // free_ev has been recorded
 
     void release() {
@@ -176,6 +178,7 @@ struct WorkSet {
         hfree(film); hfree(acc);
         if (fork_ev) (void)hipEventDestroy(fork_ev);
         if (free_ev) (void)hipEventDestroy(free_ev);
+        if (call_ev) (void)hipEventDestroy(call_ev);
         *this = WorkSet();
     }
 };
@@ -332,6 +335,21 @@ struct spt_scene_t {
 
 namespace {
 
+// Makes the scene's device current for one API call and restores the
+// caller's afterwards: a scene's arrays, streams and events live on the device
+// it was committed on, whatever device the calling thread has current (the C++
+// host destroys every rank's scene from one thread).
+struct DeviceGuard {
+    int prev = -1;
+    bool switched = false;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != device) switched = hipSetDevice(device) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (switched) (void)hipSetDevice(prev);
+    }
+};
+
 // (see PublicUse) caller holds sc->mu
 spt_status quiesce_scene(spt_scene_t* sc) {
     for (WorkSet& w : sc->ws.sets)
@@ -405,8 +423,28 @@ Camera make_camera(const spt_render_params& p) {
 
 // A set's buffers for this render; a buffer that must grow is freed only after
 // the last render that used the set has finished with it.
+// A sub-wavefront stream of the library's own.  With own_queue, a full CU
+// mask: HIP gives a CU-masked stream a hardware queue of its own instead of
+// one of the GPU_MAX_HW_QUEUES the process's streams share, so the two working
+// sets' sub-wavefronts never serialise behind each other or behind the
+// caller's streams on a shared queue.  Falls back to a plain
+// non-blocking stream if the runtime refuses the mask.
+hipError_t create_sub_stream(hipStream_t* s, bool own_queue) {
+    if (own_queue) {
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+            std::vector<uint32_t> mask(((uint32_t)cus + 31u) / 32u, 0xffffffffu);
+            if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+            if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) return hipSuccess;
+            (void)hipGetLastError();
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uint32_t planes, size_t film_bytes,
-                            size_t acc_floats) {
+                            size_t acc_floats, bool own_queues) {
     bool quiet = !ws.used;
     const auto quiesce = [&]() -> spt_status {
         if (!quiet) HIP_TRY(hipEventSynchronize(ws.free_ev));
@@ -432,7 +470,15 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
         for (auto& e : b.count_ev)
             if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (!b.join_ev) HIP_TRY(hipEventCreateWithFlags(&b.join_ev, hipEventDisableTiming));
-        if (k > 0 && !b.stream) HIP_TRY(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
+        if (b.stream && b.own_queue != own_queues) {  // the stream kind changed (spt_config.sub_queues)
+            if ((st = quiesce())) return st;
+            HIP_TRY(hipStreamDestroy(b.stream));
+            b.stream = nullptr;
+        }
+        if (!b.stream) {
+            HIP_TRY(create_sub_stream(&b.stream, own_queues));
+            b.own_queue = own_queues;
+        }
     }
     if (film_bytes > ws.film_cap) {
         if ((st = quiesce())) return st;
@@ -450,6 +496,7 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
     }
     if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
     if (!ws.free_ev) HIP_TRY(hipEventCreateWithFlags(&ws.free_ev, hipEventDisableTiming));
+    if (!ws.call_ev) HIP_TRY(hipEventCreateWithFlags(&ws.call_ev, hipEventDisableTiming));
     return SPT_OK;
 }
 
@@ -671,6 +718,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(drain_casts, 0, 64)
     CFG_RANGE(fit_streams, 1, kMaxStreams)
     CFG_RANGE(fit_paths, 0, 1ull << 31)
+    CFG_RANGE(sub_queues, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -996,6 +1044,7 @@ spt_status spt_scene_create_cfg(const int32_t* pos_tri, const float* pos, uint64
 
 spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t nmat) {
     if (!sc || !albedo_rgb || nmat == 0) return fail(SPT_ERR_INVALID, "spt_scene_set_albedo: bad arguments");
+    DeviceGuard dg(sc->device);
     float* d = nullptr;
     HIP_TRY(hipMalloc((void**)&d, sizeof(float) * 3 * nmat));
     HIP_TRY(hipMemcpy(d, albedo_rgb, sizeof(float) * 3 * nmat, hipMemcpyHostToDevice));
@@ -1016,6 +1065,7 @@ spt_status spt_scene_set_albedo(spt_scene sc, const float* albedo_rgb, uint32_t 
 
 spt_status spt_scene_set_emission(spt_scene sc, const float* emission_rgb, uint32_t nmat) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_emission: NULL scene");
+    DeviceGuard dg(sc->device);
     std::lock_guard<std::mutex> lk(sc->mu);
     spt_status qs = quiesce_scene(sc);  // queued renders may still read the old table
     if (qs) return qs;
@@ -1065,8 +1115,9 @@ void spt_default_config(spt_config* c) {
     c->drain_q8 = kDefaultDrainQ8;
     c->drain_grid_q8 = 0;
     c->drain_casts = kDefaultDrainCasts;
-    c->fit_streams = 1;
+    c->fit_streams = 2;
     c->fit_paths = kDefaultFitPaths;
+    c->sub_queues = 1;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1092,6 +1143,7 @@ spt_status spt_scene_get_config(spt_scene sc, spt_config* out) {
 
 spt_status spt_scene_set_texture(spt_scene sc, uint32_t material, const float* rgb, uint32_t width, uint32_t height) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_texture: NULL scene");
+    DeviceGuard dg(sc->device);
     if (rgb && (width == 0 || height == 0)) return fail(SPT_ERR_INVALID, "spt_scene_set_texture: empty image");
     if (rgb && (uint64_t)width * height > (1ull << 26))
         return fail(SPT_ERR_LIMIT, "spt_scene_set_texture: %u x %u texels exceeds 2^26", width, height);
@@ -1146,6 +1198,7 @@ spt_status upload_textures(spt_scene_t* sc) {
 
 spt_status spt_scene_set_spheres(spt_scene sc, const float* center_radius, const int32_t* mat_id, uint32_t n) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: NULL scene");
+    DeviceGuard dg(sc->device);
     if (n > 256) return fail(SPT_ERR_LIMIT, "spt_scene_set_spheres: %u spheres (at most 256)", n);
     if (n && !center_radius) return fail(SPT_ERR_INVALID, "spt_scene_set_spheres: NULL spheres");
     for (uint32_t k = 0; k < n; k++) {
@@ -1173,6 +1226,7 @@ spt_status spt_scene_set_spheres(spt_scene sc, const float* center_radius, const
 
 spt_status spt_scene_set_material_kinds(spt_scene sc, const uint32_t* kinds, uint32_t nmat) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_scene_set_material_kinds: NULL scene");
+    DeviceGuard dg(sc->device);
     for (uint32_t i = 0; kinds && i < nmat; i++)
         if (kinds[i] > SPT_MAT_GLASS) return fail(SPT_ERR_INVALID, "spt_scene_set_material_kinds: kind %u of material %u", kinds[i], i);
     std::lock_guard<std::mutex> lk(sc->mu);
@@ -1227,6 +1281,7 @@ spt_status spt_bvh_build_stats(const float* tv, uint64_t ntri, const spt_config*
 
 spt_status spt_scene_destroy(spt_scene sc) {
     if (!sc) return SPT_OK;
+    DeviceGuard dg(sc->device);
     {
         std::lock_guard<std::mutex> lk(sc->mu);
         (void)quiesce_scene(sc);  // nothing queued may still read what is freed
@@ -1515,6 +1570,7 @@ spt_status cache_check_indices(const char* path, const char* what, const CacheHe
 spt_status spt_scene_save(spt_scene sc, const char* path, const void* extra, uint64_t extra_bytes) {
     static const char* what = "spt_scene_save";
     if (!sc || !path) return fail(SPT_ERR_INVALID, "%s: NULL argument", what);
+    DeviceGuard dg(sc->device);
     if (extra_bytes && !extra) return fail(SPT_ERR_INVALID, "%s: extra is NULL with %llu bytes", what,
                                            (unsigned long long)extra_bytes);
     std::lock_guard<std::mutex> lk(sc->mu);
@@ -1740,6 +1796,7 @@ spt_status spt_intersect(spt_scene sc, const spt_rays* rays, const uint8_t* mask
     // a consistent snapshot of the device arrays and knobs, launched and
     // recorded under the mutex: a scene mutator waits for this launch before it
     // frees an array the snapshot holds (quiesce_scene)
+    DeviceGuard dg(sc->device);
     std::lock_guard<std::mutex> lock(sc->mu);
     a.sc = sc->dev();
     a.refill_idle = sc->cfg.public_refill_idle;
@@ -1765,6 +1822,7 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
         return fail(SPT_ERR_INVALID, "spt_hit_info_compute: mask_size %u must be 1 or n=%u", mask_size, n);
     if (sc->ntri == 0 && sc->nsph == 0) return SPT_OK;
     HitInfoArgs a;
+    DeviceGuard dg(sc->device);
     std::lock_guard<std::mutex> lock(sc->mu);  // as spt_intersect: launched and recorded under the mutex
     a.sc = sc->dev();
     a.ox = rays->ox; a.oy = rays->oy; a.oz = rays->oz;
@@ -1781,7 +1839,7 @@ spt_status spt_hit_info_compute(spt_scene sc, const spt_rays* rays, const spt_hi
     return record_public_use(sc, (hipStream_t)stream);
 }
 
-spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* film_dev, void* stream_,
+spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* film_dev, void* caller_,
                             uint64_t* ticket_out) {
     const double wall0 = now_ms();
     if (!sc || !pp || !ticket_out) return fail(SPT_ERR_INVALID, "spt_render: NULL argument");
@@ -1795,10 +1853,14 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         return fail(SPT_ERR_INVALID, "spt_render: bad tile (%u of %u, %u rows/group)", p.tile_index, p.tile_count,
                     p.rows_per_group);
     if (p.rng_order > 1) return fail(SPT_ERR_INVALID, "spt_render: rng_order must be 0 or 1");
-    hipStream_t stream = (hipStream_t)stream_;
+    // The caller's stream orders the render with the caller's work (it starts
+    // after what was queued there, and what is queued there next waits for
+    // it); the render itself runs on its working set's own streams.
+    const hipStream_t caller = (hipStream_t)caller_;
     const uint32_t rows = spt_tile_rows(p.height, p.tile_index, p.tile_count, p.rows_per_group, nullptr, 0);
     const uint64_t P = (uint64_t)rows * p.width;
     if (P != 0 && !film_dev) return fail(SPT_ERR_INVALID, "spt_render: NULL film");
+    DeviceGuard dg(sc->device);
     std::lock_guard<std::mutex> lock(sc->mu);  // the scene's one workspace
     RenderSlot* slot = nullptr;
     spt_status st = render_slot(sc->ws, &slot);
@@ -1885,7 +1947,18 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // sub-wavefront's launch tail overlaps the others' work.
     // Measured on the headline config: 1 stream 1982, 2: 2649, 3: 2769, 4: 2791 Mpaths/s
     // (4 = the box's hardware queues per process, GPU_MAX_HW_QUEUES).
-    int K = fused ? 1 : fit ? (int)cfg.fit_streams : (int)cfg.streams;
+    // The set's streams get hardware queues of their own (CU-masked streams,
+    // spt_config.sub_queues) unless the caller renders on the legacy null
+    // stream: CU-masked streams are blocking, and every null-stream operation
+    // (the event this render waits for, the one the caller waits on) would
+    // wait for them — the other working set's render included — so renders
+    // queued there would not overlap.  Such a set uses plain non-blocking
+    // streams, which share the process's GPU_MAX_HW_QUEUES, and a fitting job
+    // then runs on one sub-wavefront: more would share queues with the other
+    // set's and serialise behind them.
+    const bool null_caller = caller == nullptr || caller == hipStreamLegacy || caller == hipStreamPerThread;
+    const bool own_queues = cfg.sub_queues != 0 && !null_caller;
+    int K = fused ? 1 : fit ? (own_queues ? (int)cfg.fit_streams : 1) : (int)cfg.streams;
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
@@ -1902,10 +1975,16 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     const uint32_t chunk = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
     rs.paths_in_flight = (uint32_t)C;
-    WorkSet& ws = sc->ws.pick_set(stream);
+    WorkSet& ws = sc->ws.pick_set(caller);
     ws.last_ticket = sc->ws.next_ticket;
-    st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P);
+    st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P,
+                          own_queues);
     if (st) return st;
+    // the set's stream 0 (its own): the render's first and last launches, the
+    // fork and join of the other sub-wavefronts
+    const hipStream_t stream = ws.sub[0].stream;
+    HIP_TRY(hipEventRecord(ws.call_ev, caller));
+    HIP_TRY(hipStreamWaitEvent(stream, ws.call_ev, 0));
     JumpTable* jtab = nullptr;
     if ((st = ensure_jumps(sc->ws, stream, p.spp, p.max_depth, p.rng_initstate, &jtab))) return st;
     const PcgJump* jumps = jtab->dev;
@@ -1935,7 +2014,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         return hipMemsetAsync(ws.film, 0xff, (size_t)ns * film_unit * P, stream);
     };
     hipStream_t strm[kMaxStreams];
-    for (int k = 0; k < K; k++) strm[k] = k == 0 ? stream : ws.sub[k].stream;
+    for (int k = 0; k < K; k++) strm[k] = ws.sub[k].stream;
     // the set's previous render (another stream, perhaps) must be done with it
     if (ws.used) HIP_TRY(hipStreamWaitEvent(stream, ws.free_ev, 0));
     // From here on work is queued on the set's streams.  Any early return
@@ -1944,7 +2023,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // render that picks this set waits for whatever this one left running.
     struct EnqueueGuard {
         WorkSet& ws;
-        hipStream_t stream;
+        hipStream_t stream, caller;
         JumpTable& jt;
         int set = 0;
         int K = 1;
@@ -1957,10 +2036,11 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             }
             (void)hipEventRecord(ws.free_ev, stream);
             (void)hipEventRecord(jt.ev[set], stream);
+            (void)hipStreamWaitEvent(caller, ws.free_ev, 0);
             jt.ev_used[set] = true;
             ws.used = true;
         }
-    } guard{ws, stream, *jtab, set_idx, K};
+    } guard{ws, stream, caller, *jtab, set_idx, K};
     HIP_TRY(hipMemsetAsync(slot->dev, 0, sizeof(Stats), stream));
     // time origin for the isect launch intervals (their union = isect busy time)
     slot->timing = timing;
@@ -2011,7 +2091,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         IsectQueueArgs& I = ia[k];
         I.sc = sc->dev();
         I.hits = (float4*)b.hits;
-        I.nt = queue_nt;
+        I.nt = queue_nt && !trav_stats;
         I.max_depth = p.max_depth;
         I.trav_stats = trav_stats ? slot->dev->trav : nullptr;
         I.next = &b.cnt->isect_next;
@@ -2351,12 +2431,15 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     HIP_TRY(hipEventRecord(ws.free_ev, stream));  // every sub-stream joined `stream` before the resolve
     HIP_TRY(hipEventRecord(jtab->ev[set_idx], stream));  // this render is done with the jump table
     jtab->ev_used[set_idx] = true;
+    HIP_TRY(hipStreamWaitEvent(caller, ws.free_ev, 0));  // the caller's next work sees the film
     ws.used = true;
     guard.armed = false;
     rs.iterations = iters;
     rs.drain_launches = drain_launches;
     rs.work_order = pixel_major ? SPT_WORK_PIXEL_MAJOR : SPT_WORK_SAMPLE_MAJOR;
-    rs.queue_cache = fused ? 0u : (queue_nt ? SPT_QUEUE_CACHE_STREAM : SPT_QUEUE_CACHE_CACHED);
+    // the policy that ran: every queue kernel has a non-temporal instance,
+    // except the traversal-statistics isect variant (diagnostics)
+    rs.queue_cache = fused ? 0u : (queue_nt && !trav_stats ? SPT_QUEUE_CACHE_STREAM : SPT_QUEUE_CACHE_CACHED);
     rs.streams = (uint32_t)K;
     rs.fused = fused ? 1u : 0u;
     slot->regen_base = std::min<uint64_t>(C, P * p.spp);
@@ -2368,6 +2451,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
 
 spt_status spt_render_wait(spt_scene sc, uint64_t ticket, spt_render_stats* stats_out) {
     if (!sc) return fail(SPT_ERR_INVALID, "spt_render_wait: NULL scene");
+    DeviceGuard dg(sc->device);
     std::lock_guard<std::mutex> lock(sc->mu);
     RenderSlot& r = sc->ws.slots[ticket % kRenderSlots];
     if (!r.pending || r.ticket != ticket)

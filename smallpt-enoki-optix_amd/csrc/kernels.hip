@@ -1692,7 +1692,9 @@ uint32_t isect_queue_lanes(const IsectQueueArgs& a) {
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
-    if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false>(a, grid_items, s);
+    if (!a.sc.nodes8)
+        return a.nt ? launch_isect_queue_t<Tracer, false, false, true>(a, grid_items, s)
+                    : launch_isect_queue_t<Tracer, false>(a, grid_items, s);
     if (a.nt)
         return a.sc.node6 ? launch_isect_queue_t<Tracer6, false, false, true>(a, grid_items, s)
                           : launch_isect_queue_t<Tracer8, false, false, true>(a, grid_items, s);
@@ -1762,8 +1764,10 @@ hipError_t launch_shade(const ShadeArgs& a, int mode, uint32_t grid_items, hipSt
     if (grid_items == 0) return hipSuccess;
     const dim3 g(blocks_for(grid_items, kShadeBlock)), b(kShadeBlock);
     const bool spt = a.sc.nsph || a.sc.nkind;  // never in unit mode (spt_render)
-    if (a.nt && !spt) {  // non-temporal queue accesses (spt_config.queue_cache)
-        if (mode == kModeEmit) hipLaunchKernelGGL((shade_kernel<kModeEmit, false, true>), g, b, 0, s, a);
+    if (a.nt) {  // non-temporal queue accesses (spt_config.queue_cache), every instance
+        if (mode == kModeEmit && spt) hipLaunchKernelGGL((shade_kernel<kModeEmit, true, true>), g, b, 0, s, a);
+        else if (mode == kModeEmit) hipLaunchKernelGGL((shade_kernel<kModeEmit, false, true>), g, b, 0, s, a);
+        else if (mode == kModeAlbedo && spt) hipLaunchKernelGGL((shade_kernel<kModeAlbedo, true, true>), g, b, 0, s, a);
         else if (mode == kModeAlbedo) hipLaunchKernelGGL((shade_kernel<kModeAlbedo, false, true>), g, b, 0, s, a);
         else hipLaunchKernelGGL((shade_kernel<kModeUnit, false, true>), g, b, 0, s, a);
         return hipGetLastError();

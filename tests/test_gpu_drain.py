@@ -69,7 +69,10 @@ def test_drain_bitexact(mesh, mode, q8, casts, streams, wf, monkeypatch):
     knobs = dict(drain_q8=q8, drain_casts=casts, streams=streams, fit_streams=streams)
     s = gpu_scene(mesh, mat, **knobs)
     kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
-    film, st = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, **kw))
+    # on a side stream: the set's own (CU-masked) streams, fit_streams sub-wavefronts
+    # (a caller's null stream gets plain streams and one sub-wavefront for a fitting job)
+    side = torch.cuda.Stream()
+    film, st = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, **kw), stream=side)
     torch.cuda.synchronize()
     osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
                         sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
@@ -84,6 +87,12 @@ def test_drain_bitexact(mesh, mode, q8, casts, streams, wf, monkeypatch):
         assert st["drained_paths"] > 0
     if q8 and casts and not wf:  # the job fits: the drain runs `casts` casts after the start
         assert st["drained_paths"] > 0 and st["streams"] == streams
+    # the same render from the null stream: plain streams, one sub-wavefront when it fits
+    if q8 == 1024 and casts == 1 and not wf:
+        film0, st0 = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, **kw))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(film0.cpu().numpy(), ref)
+        assert st0["streams"] == 1
 
 
 def test_drain_sample_chunks(mesh, monkeypatch):

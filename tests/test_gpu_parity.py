@@ -367,6 +367,17 @@ def test_queue_cache_bitexact(small, cache):
     ref_u, _ = O.OracleScene(m).render(O.reference_params(w, h, spp, depth))
     np.testing.assert_array_equal(got_u, ref_u)
     assert st_u["queue_cache"] == cache
+    # smallpt spheres with mirror / glass kinds: the kSpt shade instance honours the policy too
+    sph = np.array([[0.0, 0.6, 0.0, 0.35]], np.float32)
+    kinds = np.zeros(len(albedo), np.uint32)
+    kinds[2] = 2
+    s.backend.set_spheres(sph, np.array([2], np.int32))
+    s.backend.set_material_kinds(kinds)
+    got_s, st_s = render(s, w, h, spp, depth, pipeline="wavefront", wavefront_paths=3000)
+    ref_s, _ = O.OracleScene(m, albedo=albedo, emission=emi, spheres=sph, sphere_mat=[2], kinds=kinds).render(
+        O.reference_params(w, h, spp, depth))
+    np.testing.assert_array_equal(got_s, ref_s)
+    assert st_s["queue_cache"] == cache
     # AUTO on this small scene (< 256 MiB on the device): cached
     a = sptamd.Scene()
     a.add_arrays(m)

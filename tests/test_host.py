@@ -162,7 +162,7 @@ def test_config_defaults_and_env_overrides():
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
     assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 0            # spt.h docs = code
     assert (c.drain_q8, c.drain_grid_q8, c.drain_casts) == (1024, 0, 1)
-    assert (c.fit_streams, c.fit_paths) == (1, 1 << 27)
+    assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 27, 1)
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
     assert (d.drain_q8, d.drain_casts, d.fit_paths) == (0, 4, 0)
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16

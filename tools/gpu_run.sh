@@ -52,6 +52,7 @@ for s in "$@"; do
     pmcshade1) run pmcshade1 600 env SPT_STREAMS=1 KERNEL=shade_kernel bash tools/pmc_sweep.sh gpurun_out/pmc_shade1 "FETCH_SIZE" "WRITE_SIZE" ;;
     pmc1s) run pmc1s 900 env SPT_STREAMS=1 CONFIG=1 bash tools/pmc_isect.sh gpurun_out/pmc1s ;;
     proff) run proff 600 rocprofv3 --kernel-trace --stats -d gpurun_out/proff -o run --output-format csv -- python bench.py --pipeline fused --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcd1|pmcd4) c=${s#pmcd}; run $s 900 env CONFIG=$c KERNEL=drain bash tools/pmc_isect.sh gpurun_out/pmc ;;
     pmcf) run pmcf 900 env CONFIG=1 PIPE=fused bash tools/pmc_isect.sh gpurun_out/pmc ;;
     prof1s) run prof1s 600 env SPT_STREAMS=1 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1s -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     trav) run trav 600 python tools/trav_stats.py ;;
@@ -62,6 +63,7 @@ for s in "$@"; do
     drainsweep) for dq in ${DRAINS:-0 256 512 1024 2048}; do run drain$dq 300 env SPT_DRAIN_Q8=$dq python tools/tile_sim.py --tiles 1 2 4 8 --pipeline wavefront --steps 8; done ;;
     sweep) run sweep 600 python tools/tile_sim.py --tiles ${TILES:-1 2 4 8} --pipeline ${PIPE:-wavefront} --steps ${STEPS:-8} --sweep $SWEEP ;;
     matrix) i=0; IFS=';' read -ra CFGS <<< "$MATRIX"; for c in "${CFGS[@]}"; do i=$((i+1)); run matrix$i 300 env ${c//,/ } python tools/tile_sim.py --tiles ${TILES:-1 2 4 8} --pipeline ${PIPE:-wavefront} --steps ${STEPS:-40} --sweep REP=${REPS:-1,2} TAG=m$i; done ;;
+    benchm) i=0; IFS=';' read -ra CFGS <<< "$MATRIX"; for c in "${CFGS[@]}"; do i=$((i+1)); run benchm$i 400 env ${c//,/ } python bench.py --config ${CONFIG:-1} --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline; done ;;
     tilesimw) run tilesimw 400 python tools/tile_sim.py --tiles 1 2 4 8 --pipeline wavefront --timing ;;
     tilesima) run tilesima 400 python tools/tile_sim.py --tiles 1 2 4 8 --timing ;;
     tilesim) run tilesim 400 python tools/tile_sim.py ;;

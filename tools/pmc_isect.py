@@ -57,9 +57,19 @@ def main(out, key, log, *paths):
     b = bench_line(log)
     roof = b["roofline"]
     # units per launch (ray casts for isect_queue_kernel, paths for the fused
-    # kernel): the bench line's algorithmic bytes per launch / bytes per unit
-    unit = "path" if roof.get("unit_of_work") == "path" else "cast"
-    casts = roof["algorithmic_bytes_per_launch"] / roof["bytes_per_unit"]
+    # kernel and the drain): from the bench line's per-kernel table when it
+    # names this kernel (the drain: ray casts and drained paths per launch),
+    # else its algorithmic bytes per launch / bytes per unit
+    kt = {k: v for k, v in roof.get("kernels", {}).items() if kernel in k}
+    cast_per_launch = None
+    if kt:
+        (kname, kv), = kt.items()
+        cast_per_launch = kv["casts_per_step"] / max(kv["launches_per_step"], 1e-9)
+        unit = "cast" if kv["unit"] == "ray cast" else "path"
+        casts = kv["units_per_step"] / max(kv["launches_per_step"], 1e-9)
+    else:
+        unit = "cast" if roof.get("unit_of_work") == "ray cast" else "path"
+        casts = roof["algorithmic_bytes_per_launch"] / roof["bytes_per_unit"]
     rec = {"kernel": kernel, "workload": b["config"]["workload"], "streams": b["config"]["streams"],
            "pipeline": b["config"].get("pipeline"), "work_order": b["config"].get("work_order"),
            # the library build the passes measured (spt_build_id): bench.py uses
@@ -70,16 +80,22 @@ def main(out, key, log, *paths):
            "hw_queues": b["config"].get("hw_queues"),
            f"{unit}s_per_launch": casts, "dispatches": {c: len(v) for c, v in per.items()}, "per_launch": mean,
            "source": [os.path.relpath(p) for p in paths]}
+    if cast_per_launch:
+        rec["casts_per_launch"] = cast_per_launch
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
         t = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
         rec["traffic_bytes_per_launch"] = t
         rec[f"traffic_bytes_per_{unit}"] = t / casts
+        if cast_per_launch and unit != "cast":
+            rec["traffic_bytes_per_cast"] = t / cast_per_launch
         rec[f"read_bytes_per_{unit}"] = 2.0 * mean["FETCH_SIZE"] * 1024.0 / casts
         rec[f"write_bytes_per_{unit}"] = mean["WRITE_SIZE"] * 1024.0 / casts
         rec["traffic_correction"] = "reads x2 (gfx950 FETCH_SIZE half-count, MI355X_MICROARCH.md HBM); estimate"
     if "SQ_INSTS_VALU" in mean:
         rec["valu_insts_per_launch"] = mean["SQ_INSTS_VALU"]
         rec[f"valu_insts_per_{unit}"] = mean["SQ_INSTS_VALU"] / casts
+        if cast_per_launch and unit != "cast":
+            rec["valu_insts_per_cast"] = mean["SQ_INSTS_VALU"] / cast_per_launch
     if "TCC_HIT_sum" in mean:
         rec["l2_hit_rate"] = mean["TCC_HIT_sum"] / max(1.0, mean["TCC_HIT_sum"] + mean.get("TCC_MISS_sum", 0.0))
     if "SQ_WAVE_CYCLES" in mean:

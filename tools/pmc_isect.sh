@@ -3,7 +3,7 @@
 # pass (kernel-trace only, each under its own time limit), then
 # tools/pmc_isect.py merges the per-cast figures into OUTDIR/isect_pmc.json
 # under "config<N>".
-#   usage: CONFIG=1 [PIPE=fused] tools/pmc_isect.sh OUTDIR      (CONFIG default 1)
+#   usage: CONFIG=1 [PIPE=fused] [KERNEL=drain] tools/pmc_isect.sh OUTDIR      (CONFIG default 1)
 # PIPE=fused: the fused trace+shade kernel (--pipeline fused), key "config<N>_fused".
 set -u
 out=${1:-gpurun_out/pmc}
@@ -12,6 +12,8 @@ pipe=${PIPE:-auto}
 regex=isect_queue
 key=config$cfg
 if [ "$pipe" = fused ]; then regex=render_fused; key=config${cfg}_fused; fi
+# KERNEL=drain: the wavefront's drain (render_fused_kernel<drain>), key "config<N>_drain"
+if [ "${KERNEL:-isect}" = drain ]; then regex=render_fused; key=config${cfg}_drain; fi
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p "$out"
 export TMPDIR=/tmp
