@@ -79,10 +79,10 @@ enum {
     SPT_FLAG_TIMING = 1u,          /* record HIP events around every isect launch (isect_ms) */
     SPT_FLAG_TRAVERSAL_STATS = 2u, /* count node visits / triangle tests (slower variant; wavefront) */
     SPT_FLAG_FUSED = 4u,           /* one persistent trace+shade kernel per sample chunk */
-    SPT_FLAG_WAVEFRONT = 8u,       /* isect / shade / refill kernels over path queues
-                                      (neither flag: spt_config.pipeline; AUTO = fused iff
-                                      the tile has at most fused_max_paths = 32M paths, or
-                                      at most wavefront_paths when that is set) */
+    SPT_FLAG_WAVEFRONT = 8u,       /* isect / shade / refill kernels over path queues, with the
+                                      drain (neither flag: spt_config.pipeline; AUTO = fused iff
+                                      the tile has at most fused_max_paths paths, 0 by default,
+                                      or at most wavefront_paths when that is set) */
     SPT_FLAG_TIMING_ALL = 16u      /* with SPT_FLAG_TIMING: also shade / refill / resolve launches */
 };
 
@@ -293,7 +293,7 @@ typedef struct spt_config {
                                        a caller's null stream (shared hardware queues)        [1..4] */
     uint64_t fit_paths;             /* a job of at most this many paths (tile px x spp) starts every
                                        path in the first refill (paths in flight = the job, unless
-                                       params.wavefront_paths is set) on fit_streams
+                                       params.wavefront_paths or config.wavefront_paths is set) on fit_streams
                                        sub-wavefronts: its last work item starts at once, so the
                                        drain takes over drain_casts casts later; 2^27 (about 11 GB
                                        of queues at most), 0: off               */

@@ -1938,7 +1938,9 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // streams overlap without sub-wavefront streams of their own (DESIGN.md §6:
     // stable at the box's four hardware queues, where four sub-wavefront
     // streams per working set could share a queue with the other set's).
-    const bool fit = !fused && !p.wavefront_paths && cfg.fit_paths && cfg.drain_q8 && P * p.spp <= cfg.fit_paths;
+    // (an explicit paths-in-flight count, in the params or the config, wins)
+    const bool fit = !fused && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths && cfg.fit_paths &&
+                     cfg.drain_q8 && P * p.spp <= cfg.fit_paths;
     if (fit) C = P * p.spp;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
@@ -2168,6 +2170,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         F.sc = sc->dev();
         F.cam = cam;
         F.sample_jump = jumps;
+        F.cast_jump = jumps + p.spp;
         F.sfilm = sfilm;
         F.sflag = sflag;
         F.stats = slot->dev->stats;

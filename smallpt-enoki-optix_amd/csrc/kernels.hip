@@ -80,6 +80,9 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #ifndef SPT_FUSED_WAVES
 #define SPT_FUSED_WAVES 5  // the fused kernel: 6 (80 VGPRs, no spills in unit mode) ran 2 % slower
 #endif
+#ifndef SPT_DRAIN_WAVES
+#define SPT_DRAIN_WAVES 5  // the drain instance (the compiler then picks 80 VGPRs / 6 waves in unit mode)
+#endif
 
 // ------------------------------------------------------------- traversal
 // Triangle records (spt_internal.h): vertex i of slot s rotated by r starts at
@@ -1281,7 +1284,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 // arithmetic, same film writes, so the same bits as the queue kernels.
 template <typename Tr, int kMode, bool kDrain = false, bool kNt = false>
 __global__ __launch_bounds__(kIsectBlock)
-__attribute__((amdgpu_waves_per_eu(SPT_FUSED_WAVES, 8)))
+__attribute__((amdgpu_waves_per_eu(kDrain ? SPT_DRAIN_WAVES : SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
     extern __shared__ uint32_t lds_stack[];
@@ -1295,11 +1298,15 @@ void render_fused_kernel(FusedArgs a) {
     NoStats st;
     Tr tr;
     V3 dir = v3(0, 0, 0);
-    uint64_t rs = 0;
-    uint32_t pix = 0, gpix = 0, sample = 0, depth = 0;
+    // A lane carries no PCG32 state: the shade re-derives it at the cast's
+    // bounce draw from (pixel, sample, cast) as shade_kernel does (path_rng),
+    // and the work counters are wave-uniform (ballot counts), so the path
+    // state the traversal loop keeps live is the ray, pixel, sample, cast and
+    // throughput only (VGPRs: occupancy).
+    uint32_t pix = 0, meta = 0;  // tile pixel; sample << 8 | cast (as a queue path's q1.w)
     float thr = 1.0f, thg = 1.0f, thb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     bool busy = false, pending = false;
-    uint32_t casts = 0, conts = 0, starts = 0;
+    uint32_t casts = 0, conts = 0, starts = 0;  // wave-uniform
     // wave-uniform work pool: static share, then dynamic chunks
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
     const uint32_t wave_id = wave_uniform(blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6));
@@ -1310,10 +1317,12 @@ void render_fused_kernel(FusedArgs a) {
     while (true) {
         if ((uint32_t)__popcll(__ballot(!busy)) >= a.refill_idle) {
             // ---- shade every pending lane (shade_kernel, main.cpp:404-425)
+            casts += (uint32_t)__popcll(__ballot(pending));
+            bool cont = false;
             if (pending) {
                 pending = false;
-                casts++;
                 bool term = true;
+                const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u), sample = meta >> kMetaDepthBits;
                 TraceHit hh = tr.hit(a.sc, L);
                 if (kMode != kModeUnit && a.sc.nsph)  // smallpt's spheres after the BVH
                     trace_spheres(a.sc, tr.o, dir, kRayTmin, depth + 1 >= a.max_depth && !kEmit, hh);
@@ -1334,6 +1343,9 @@ void render_fused_kernel(FusedArgs a) {
                         lb = lb + thb * a.sc.emission[mat * 3 + 2];
                     }
                     if (depth + 1 < a.max_depth) {
+                        // the global pixel (main.cpp:379-382), for the roulette draw and the PCG32 stream
+                        const uint32_t gpix =
+                            tile_global_row(pix / a.W, a.tile_index, a.tile_count, a.rows_per_group) * a.W + pix % a.W;
                         if (kMode != kModeUnit) {
                             const V3 rf = reflectance(a.sc, mat, (uint32_t)slot, hh.u, hh.v);  // main.cpp:418
                             thr = thr * rf.x;                        // main.cpp:422
@@ -1355,9 +1367,8 @@ void render_fused_kernel(FusedArgs a) {
                             const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
                             const float4 m1 = sph ? zero : a.sc.snrm[(size_t)slot * 3 + 1];
                             const float4 m2 = sph ? zero : a.sc.snrm[(size_t)slot * 3 + 2];
-                            Pcg32 rng;
-                            rng.state = rs;
-                            rng.inc = ((uint64_t)gpix << 1u) | 1u;
+                            // at this cast's bounce draw, 4 + 2 depth past the sample's first
+                            Pcg32 rng = path_rng(gpix, a.sample_jump[sample], a.cast_jump[depth]);
                             float xi_x, xi_y;
                             draw2(rng, a.rng_order, xi_x, xi_y);   // main.cpp:413
                             const float t = hh.t, u = hh.u, v = hh.v;
@@ -1375,11 +1386,10 @@ void render_fused_kernel(FusedArgs a) {
                                 dir = scatter(a.sc, material_kind(a.sc, mat), slot, dir, hp, sn, xi_x, xi_y, wgt);
                                 thr = thr * wgt; thg = thg * wgt; thb = thb * wgt;
                             }
-                            rs = rng.state;
-                            depth++;
-                            tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit, L);
+                            meta++;  // the next cast
+                            tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 2 >= a.max_depth && !kEmit, L);
                             busy = true;
-                            conts++;
+                            cont = true;
                         }
                     }
                 }
@@ -1395,6 +1405,7 @@ void render_fused_kernel(FusedArgs a) {
                     }
                 }
             }
+            conts += (uint32_t)__popcll(__ballot(cont));
             // ---- new camera paths in free lanes (refill_kernel)
             uint64_t idle = __ballot(!busy && !pending);
             while (idle && !(drained && pool == pool_end)) {
@@ -1413,15 +1424,10 @@ void render_fused_kernel(FusedArgs a) {
                     // the next queued path (shade_kernel's reads), continued here
                     const uint32_t j = pool + rank;
                     const float4 q1 = ldq<kNt>(a.q.q1 + j), q2 = ldq<kNt>(a.q.q2 + j);
-                    const uint32_t meta = f2u(q1.w);
-                    depth = meta & ((1u << kMetaDepthBits) - 1u);
-                    sample = meta >> kMetaDepthBits;
+                    meta = f2u(q1.w);
+                    const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
                     pix = f2u(q2.w);
-                    const uint32_t lx = pix % a.W, ly = pix / a.W;
-                    gpix = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group) * a.W + lx;
                     dir = v3(q2.x, q2.y, q2.z);
-                    // at the bounce draw of this cast: 4 + 2 cast draws past the sample's first
-                    rs = path_rng(gpix, a.sample_jump[sample], a.cast_jump[depth]).state;
                     thr = thg = thb = 1.0f;
                     lr = lg = lb = 0.0f;
                     if (kMode >= kModeAlbedo) {
@@ -1440,25 +1446,25 @@ void render_fused_kernel(FusedArgs a) {
                         pending = true;
                     }
                 } else if (!kDrain && !busy && !pending && rank < take) {
+                    uint32_t sample;
                     work_item(pool + rank, a.sample0, a.pm_ns, a.P, a.pm_ns != 0, sample, pix);  // work0 = sample0 * P
                     const uint32_t lx = pix % a.W, ly = pix / a.W;  // scanline (pixel blocks: refill_kernel only)
                     const uint32_t gy = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group);
-                    gpix = gy * a.W + lx;                          // main.cpp:379-382
+                    const uint32_t gpix = gy * a.W + lx;           // main.cpp:379-382
                     Pcg32 rng = pcg_start(a.sample_jump[sample], (uint64_t)gpix);  // main.cpp:376 + the sample's draws
                     V3 o;
                     camera_ray(a.cam, rng, a.rng_order, lx, gy, o, dir);
-                    rs = rng.state;
-                    depth = 0;
+                    meta = sample << kMetaDepthBits;  // cast 0
                     thr = thg = thb = 1.0f;                        // main.cpp:391
                     lr = lg = lb = 0.0f;
                     tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit, L);
-                    starts++;
                     busy = true;
                     if (tr.finished()) {  // empty scene: a miss
                         busy = false;
                         pending = true;
                     }
                 }
+                if (!kDrain) starts += take;
                 pool += take;
                 idle = __ballot(!busy && !pending);
             }
@@ -1473,20 +1479,11 @@ void render_fused_kernel(FusedArgs a) {
     // (by the refill that follows), so only the casts after it are added;
     // every cast it traced goes to drained_casts
     if constexpr (kDrain) {
-        uint32_t dc = casts;
-#pragma unroll
-        for (uint32_t off = 32; off > 0; off >>= 1) dc += (uint32_t)__shfl_down((int)dc, off);
-        if ((threadIdx.x & 63u) == 0 && dc) atomicAdd(a.drained_casts, (unsigned long long)dc);
+        if ((threadIdx.x & 63u) == 0 && casts) atomicAdd(a.drained_casts, (unsigned long long)casts);
         casts = conts;
         starts = 0;
     }
-    // per-wave sums, one atomic per counter per wave
-#pragma unroll
-    for (uint32_t off = 32; off > 0; off >>= 1) {
-        casts += (uint32_t)__shfl_down((int)casts, off);
-        conts += (uint32_t)__shfl_down((int)conts, off);
-        starts += (uint32_t)__shfl_down((int)starts, off);
-    }
+    // the wave's counts (uniform), one atomic per counter per wave
     if ((threadIdx.x & 63u) == 0) {
         if (casts) atomicAdd(&a.stats[0], (unsigned long long)casts);
         if (conts) atomicAdd(&a.stats[1], (unsigned long long)conts);

@@ -354,7 +354,7 @@ struct FusedArgs {
     // each path's first (the refill that follows counts the queue itself).
     PathQueue q;
     const uint32_t* qcount;
-    const PcgJump* cast_jump;       // [max_depth]: jump by 4 + 2 * cast draws
+    const PcgJump* cast_jump;       // [max_depth]: jump by 4 + 2 * cast draws (both modes: the shade re-derives the state)
     uint32_t drain_below;
     uint32_t nt;                    // 1: non-temporal queue loads (spt_config.queue_cache)
     unsigned long long* drained;    // paths the drain launches took over

@@ -203,10 +203,15 @@ def test_config4_box_exit_rule_against_float64():
     osc = oracle_scene(4)
     pos = np.asarray(s.mesh["pos"], np.float32)
     so, sd = surface_rays(lambda o, d: osc.intersect(o, d, nthreads=16), pos.min(0), pos.max(0), 4_000_000, seed=3)
+    # with the round-3 ray the rule is known to act on (a Woop hit at t = 0.0015
+    # whose triangle box the ray leaves at t = 0.0003): the audit must see it
+    ko = np.array([[-0.24933969974517822], [1.7225027084350586], [8.833206176757812]], np.float32)
+    kd = np.array([[-0.3425644636154175], [0.8412052392959595], [0.4182586371898651]], np.float32)
+    so, sd = np.concatenate([ko, so], axis=1), np.concatenate([kd, sd], axis=1)
     found, accepted, worst = box_exit_audit(s.mesh["pos"], s.mesh["pos_tri"], osc, so, sd)
     print(f"city surface rays {so.shape[1]}: Woop hits {accepted}, dropped {found}, max exit/tmin {worst:.4f}")
     assert so.shape[1] > 1_000_000
     eo, ed = edge_leaving_rays(s.mesh["pos"], s.mesh["pos_tri"], 1_000_000, seed=7)
     found2, accepted2, worst2 = box_exit_audit(s.mesh["pos"], s.mesh["pos_tri"], osc, eo, ed)
     print(f"city edge-leaving rays {eo.shape[1]}: Woop hits {accepted2}, dropped {found2}, max exit/tmin {worst2:.4f}")
-    assert found + found2 > 0
+    assert found >= 1  # the known ray's drop, at least (the rule acts on few rays: DESIGN.md §2)

@@ -25,6 +25,7 @@ for s in "$@"; do
   case "$s" in
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread ;;
+    testsnx) run testsnx 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
     testsv) run testsv 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
     testsall) run testsall 900 python -m pytest tests -m gpu -q ;;
     tests2) run tests2 900 env SPT_BVH=2 python -m pytest tests -m gpu -q -x ;;
