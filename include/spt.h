@@ -303,6 +303,10 @@ typedef struct spt_config {
                                        streams, so a set bound to the legacy null stream uses plain
                                        non-blocking streams instead.  0: plain streams always
                                        (they share the process's queues)       [0..1] */
+    uint32_t drain_sort;            /* 1: a forced drain takes its queue sorted by the direction's
+                                       octant and the origin's Morton code (coherent bounce rays
+                                       per wave; wide-BVH scenes); 0: queue order.  The image does
+                                       not depend on it                                       [0..1] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -142,6 +142,11 @@ struct Sub {
     char* hits = nullptr;
     Counters* cnt = nullptr;
     hipStream_t stream = nullptr;       // the library's own stream (spt_config.sub_queues)
+    // spt_config.drain_sort: sort keys / values (in, out) over cap slots and hipcub scratch
+    uint32_t* sort_buf = nullptr;
+    size_t sort_cap = 0;
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
     bool own_queue = false;             // created with a full CU mask (spt_config.sub_queues)
     Counters* host_cnt = nullptr;       // pinned, 2 slots (counter snapshots read one batch behind)
     hipEvent_t count_ev[2] = {nullptr, nullptr};
@@ -169,7 +174,8 @@ struct WorkSet {
 
     void release() {
         for (Sub& b : sub) {
-            hfree(b.qa); hfree(b.qb); hfree(b.hits); hfree(b.cnt);
+            hfree(b.qa); hfree(b.qb); hfree(b.hits); hfree(b.cnt); hfree(b.sort_buf);
+            if (b.sort_tmp) (void)hipFree(b.sort_tmp);
             if (b.host_cnt) (void)hipHostFree(b.host_cnt);
             for (auto& e : b.count_ev) if (e) (void)hipEventDestroy(e);
             if (b.join_ev) (void)hipEventDestroy(b.join_ev);
@@ -719,6 +725,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(fit_streams, 1, kMaxStreams)
     CFG_RANGE(fit_paths, 0, 1ull << 31)
     CFG_RANGE(sub_queues, 0, 1)
+    CFG_RANGE(drain_sort, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -1118,6 +1125,7 @@ void spt_default_config(spt_config* c) {
     c->fit_streams = 2;
     c->fit_paths = kDefaultFitPaths;
     c->sub_queues = 1;
+    c->drain_sort = 0;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -2084,6 +2092,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // the drain: not with traversal counters (isect kernel only) or camera
     // paths started inside the isect launches (an experiment)
     const bool drain_on = cfg.drain_q8 != 0 && !trav_stats && !kIsectCam;
+    // spt_config.drain_sort: a forced drain takes its queue sorted (wide-BVH scenes)
+    const bool drain_sort = drain_on && cfg.drain_sort != 0 && sc->nodes8 != nullptr;
     uint64_t drain_launches = 0;
     PathQueue q[kMaxStreams][2];
     for (int k = 0; k < K; k++) {
@@ -2322,6 +2332,27 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         da[k].q = q[k][c];
                         da[k].qcount = &b.cnt->qn[c];
                         da[k].drain_below = 0xffffffffu;
+                        da[k].perm = nullptr;
+                        if (drain_sort) {  // the drain's order: by direction octant, then origin (kernels.hip)
+                            const size_t cap = b.cap;
+                            if (b.sort_cap < cap) {
+                                HIP_TRY(hipStreamSynchronize(strm[k]));  // a previous render may still sort in them
+                                hfree(b.sort_buf);
+                                if (b.sort_tmp) (void)hipFree(b.sort_tmp);
+                                b.sort_tmp = nullptr;
+                                b.sort_cap = 0;
+                                HIP_TRY(hipMalloc((void**)&b.sort_buf, sizeof(uint32_t) * 4 * cap));
+                                HIP_TRY(launch_drain_sort(sc->dev(), q[k][c], nullptr, (uint32_t)cap, nullptr, nullptr,
+                                                          nullptr, nullptr, nullptr, &b.sort_tmp_bytes, strm[k]));
+                                HIP_TRY(hipMalloc(&b.sort_tmp, std::max<size_t>(b.sort_tmp_bytes, 16)));
+                                b.sort_cap = cap;
+                            }
+                            uint32_t* kb = b.sort_buf;
+                            HIP_TRY(launch_drain_sort(sc->dev(), q[k][c], &b.cnt->qn[c], (uint32_t)b.cap, kb, kb + cap,
+                                                      kb + 2 * cap, kb + 3 * cap, b.sort_tmp, &b.sort_tmp_bytes,
+                                                      strm[k]));
+                            da[k].perm = kb + 3 * cap;
+                        }
                         if ((st = mark(4, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
                         drain_launches++;
                         // the refill's bookkeeping: the drained paths' first casts
@@ -2351,6 +2382,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         da[k].q = q[k][c];
                         da[k].qcount = &b.cnt->qn[c];
                         da[k].drain_below = drain_T[k];
+                        da[k].perm = nullptr;
                         if ((st = mark(4, strm[k], [&] { return launch_drain(da[k], mode, strm[k]); }))) return st;
                         drain_launches++;
                     }

@@ -4,6 +4,7 @@
 //
 // Replaces wavefront_isect.cu:36-112 (OptiX raygen / closest-hit / miss) and
 // the Enoki-JIT bounce loop body main.cpp:385-426.
+#include <hipcub/hipcub.hpp>
 #include <type_traits>
 
 #include "spt_internal.h"
@@ -1422,7 +1423,7 @@ void render_fused_kernel(FusedArgs a) {
                 const uint32_t take = min((uint32_t)__popcll(idle), pool_end - pool);
                 if (kDrain && !busy && !pending && rank < take) {
                     // the next queued path (shade_kernel's reads), continued here
-                    const uint32_t j = pool + rank;
+                    const uint32_t j = a.perm ? a.perm[pool + rank] : pool + rank;
                     const float4 q1 = ldq<kNt>(a.q.q1 + j), q2 = ldq<kNt>(a.q.q2 + j);
                     meta = f2u(q1.w);
                     const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
@@ -1809,6 +1810,60 @@ static hipError_t launch_drain_m(const FusedArgs& a, hipStream_t s) {
     if (a.sc.nodes8 && a.sc.node6) return launch_fused_t<Tracer6F, kMode, true, kNt>(a, s, nullptr);
     if (a.sc.nodes8) return launch_fused_t<Tracer8F, kMode, true, kNt>(a, s, nullptr);
     return launch_fused_t<Tracer, kMode, true, kNt>(a, s, nullptr);
+}
+
+// Sort key of a queued path (launch_drain_sort): its direction's octant, then
+// the Morton code of its origin on a 512^3 grid over the root node's box, so
+// that a wave's lanes take bounce rays that start near each other and head
+// the same way (the drain continues each path in its lane, so the order
+// decides which rays a wave traces together).  Slots past the count: last.
+__global__ __launch_bounds__(256) void drain_keys_kernel(DeviceScene sc, PathQueue q, const uint32_t* count,
+                                                         uint32_t cap, uint32_t* keys, uint32_t* vals) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= cap) return;
+    uint32_t key = 0xffffffffu;
+    if (i < *count) {
+        const uint4 w0 = sc.nodes8[0], w1 = sc.nodes8[1];  // the root: origin, exponents
+        uint32_t ex, ey, ez;
+        if (sc.node6) {
+            ex = (w1.y >> 16) & 0xffu; ey = w1.y >> 24; ez = w1.z >> 24;
+        } else {
+            ex = w0.w & 0xffu; ey = (w0.w >> 8) & 0xffu; ez = (w0.w >> 16) & 0xffu;
+        }
+        const float4 q1 = q.q1[i], q2 = q.q2[i];
+        const auto cell = [](float o, uint32_t p, uint32_t e) {
+            const float ext = 255.0f * u2f(e << 23);  // the root box: p + [0, 255 * 2^(e - 127)]
+            const float f = (o - u2f(p)) / ext * 512.0f;
+            return (uint32_t)fminf(fmaxf(f, 0.0f), 511.0f);
+        };
+        const auto spread = [](uint32_t v) {  // 9 bits -> every third bit
+            v = (v | (v << 16)) & 0x030000ffu;
+            v = (v | (v << 8)) & 0x0300f00fu;
+            v = (v | (v << 4)) & 0x030c30c3u;
+            v = (v | (v << 2)) & 0x09249249u;
+            return v;
+        };
+        const uint32_t m = spread(cell(q1.x, w0.x, ex)) | spread(cell(q1.y, w0.y, ey)) << 1 |
+                           spread(cell(q1.z, w0.z, ez)) << 2;
+        const uint32_t oct = (q2.x < 0.0f ? 1u : 0u) | (q2.y < 0.0f ? 2u : 0u) | (q2.z < 0.0f ? 4u : 0u);
+        key = oct << 27 | m;
+    }
+    keys[i] = key;
+    vals[i] = i;
+}
+
+hipError_t launch_drain_sort(const DeviceScene& sc, const PathQueue& q, const uint32_t* count, uint32_t cap,
+                             uint32_t* keys, uint32_t* vals, uint32_t* keys_out, uint32_t* perm, void* tmp,
+                             size_t* tmp_bytes, hipStream_t s) {
+    if (!tmp)
+        return hipcub::DeviceRadixSort::SortPairs(nullptr, *tmp_bytes, keys, keys_out, vals, perm, (int)cap, 0, 30, s);
+    if (!sc.nodes8 || cap == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(drain_keys_kernel, dim3(blocks_for(cap, 256)), dim3(256), 0, s, sc, q, count, cap, keys, vals);
+    hipError_t e = hipGetLastError();
+    if (e) return e;
+    // 30 key bits: the octant above the 27-bit Morton code (an empty slot's
+    // all-ones key sorts after every real one in its low 30 bits too)
+    return hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, keys, keys_out, vals, perm, (int)cap, 0, 30, s);
 }
 
 hipError_t launch_drain(const FusedArgs& a, int mode, hipStream_t s) {

@@ -359,6 +359,7 @@ struct FusedArgs {
     uint32_t nt;                    // 1: non-temporal queue loads (spt_config.queue_cache)
     unsigned long long* drained;    // paths the drain launches took over
     unsigned long long* drained_casts;  // ray casts the drain launches traced
+    const uint32_t* perm;           // null, or the order the drain takes queue slots in (launch_drain_sort)
 };
 
 struct HitInfoArgs {
@@ -437,6 +438,13 @@ hipError_t launch_fused(const FusedArgs& a, int mode, hipStream_t s, uint32_t* l
 // queue (FusedArgs drain fields); runs only when the queue holds fewer than
 // drain_below paths.  grid_q8 scales the chip-wide persistent grid.
 hipError_t launch_drain(const FusedArgs& a, int mode, hipStream_t s);
+// spt_config.drain_sort: the drain's order — a queue's `cap` slots sorted by
+// (direction octant, Morton code of the origin in the scene box) into perm
+// (slots past *count sort last).  tmp / tmp_bytes: hipcub scratch; with a
+// null tmp only *tmp_bytes is set (the size to allocate).
+hipError_t launch_drain_sort(const DeviceScene& sc, const PathQueue& q, const uint32_t* count, uint32_t cap,
+                             uint32_t* keys, uint32_t* vals, uint32_t* keys_out, uint32_t* perm, void* tmp,
+                             size_t* tmp_bytes, hipStream_t s);
 // Lanes of the persistent isect grid a launch with these arguments gets (the
 // drain threshold is counted in them).
 uint32_t isect_queue_lanes(const IsectQueueArgs& a);

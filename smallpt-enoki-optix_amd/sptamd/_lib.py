@@ -123,7 +123,8 @@ class Config(ctypes.Structure):
                 ("public_persistent", c_uint32), ("public_refill_idle", c_uint32), ("pack_groups", c_uint32),
                 ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32),
                 ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32),
-                ("fit_streams", c_uint32), ("fit_paths", c_uint64), ("sub_queues", c_uint32)]
+                ("fit_streams", c_uint32), ("fit_paths", c_uint64), ("sub_queues", c_uint32),
+                ("drain_sort", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -253,6 +254,7 @@ _ENV_CONFIG = {
     "SPT_FIT_STREAMS": ("fit_streams", int),
     "SPT_FIT_PATHS": ("fit_paths", int),
     "SPT_SUB_QUEUES": ("sub_queues", int),
+    "SPT_DRAIN_SORT": ("drain_sort", int),
 }
 
 

@@ -95,6 +95,25 @@ def test_drain_bitexact(mesh, mode, q8, casts, streams, wf, monkeypatch):
         assert st0["streams"] == 1
 
 
+@pytest.mark.parametrize("mode", ["unit", "emit_spheres"])
+def test_drain_sorted_bitexact(mesh, mode, monkeypatch):
+    """spt_config.drain_sort: the forced drain takes its queue sorted by
+    direction octant and origin (launch_drain_sort); order only, same bits."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, mode)
+    s = gpu_scene(mesh, mat, drain_sort=1)
+    kw = dict(rr_start_depth=3)
+    side = torch.cuda.Stream()
+    film, st = s.render(sptamd.make_params(W, H, SPP, D, **kw), stream=side)
+    torch.cuda.synchronize()
+    osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
+                        sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
+    ref, casts = osc.render(O.reference_params(W, H, SPP, D, **kw))
+    np.testing.assert_array_equal(film.cpu().numpy(), ref)
+    assert st["ray_casts"] == casts and st["drained_paths"] > 0
+
+
 def test_drain_sample_chunks(mesh, monkeypatch):
     """Several film chunks (film_budget_bytes): each chunk's queue drains."""
     for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
