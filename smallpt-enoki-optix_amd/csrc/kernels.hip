@@ -81,8 +81,16 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #ifndef SPT_FUSED_WAVES
 #define SPT_FUSED_WAVES 5  // the fused kernel: 6 (80 VGPRs, no spills in unit mode) ran 2 % slower
 #endif
+// The drain: the unit-mode instance for scenes the caches hold (queue accesses
+// cached) at 7 waves (72 VGPRs, 8 B of scratch): config 1 +4 % (5404 vs 5216);
+// the streamed-queue instance (scenes beyond the Infinity Cache) at the
+// compiler's 6: config 4 at 7 waves -2 % (profiles/r05_exp/ab_diet_waves_sort.log);
+// albedo / emitter modes keep the fused kernel's budget (they would spill).
 #ifndef SPT_DRAIN_WAVES
-#define SPT_DRAIN_WAVES 5  // the drain instance (the compiler then picks 80 VGPRs / 6 waves in unit mode)
+#define SPT_DRAIN_WAVES 7
+#endif
+#ifndef SPT_DRAIN_WAVES_NT
+#define SPT_DRAIN_WAVES_NT 6
 #endif
 
 // ------------------------------------------------------------- traversal
@@ -1285,7 +1293,8 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 // arithmetic, same film writes, so the same bits as the queue kernels.
 template <typename Tr, int kMode, bool kDrain = false, bool kNt = false>
 __global__ __launch_bounds__(kIsectBlock)
-__attribute__((amdgpu_waves_per_eu(kDrain ? SPT_DRAIN_WAVES : SPT_FUSED_WAVES, 8)))
+__attribute__((amdgpu_waves_per_eu(kDrain && kMode == kModeUnit ? (kNt ? SPT_DRAIN_WAVES_NT : SPT_DRAIN_WAVES)
+                                                                  : SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
     extern __shared__ uint32_t lds_stack[];
