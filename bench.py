@@ -454,13 +454,17 @@ def main():
                 busy_ms=agg["isect_busy_ms"], launches=isect_launches, sum_ms=agg["isect_ms"], casts=isect_casts,
                 basis="algorithmic bytes of all isect launches / union of their intervals (isect busy)")
             if agg["drain_launches"]:
+                # SURVEY §8(d)'s per-cast figure, as for the isect kernel: the drain
+                # traces (and shades) ray casts; what it moves per cast — the queued
+                # path read once, its film write — is kernel_bytes_per_unit
+                moved = agg["drained_paths"] * (queue_b + film_b) / max(agg["drained_casts"], 1)
                 kernels["render_fused_kernel<drain>"] = dict(
-                    units=agg["drained_paths"], unit="drained path", bytes_per_unit=queue_b + film_b,
-                    kernel_bytes_per_unit=queue_b + film_b, bytes=agg["drained_paths"] * (queue_b + film_b),
+                    units=agg["drained_casts"], unit="ray cast", bytes_per_unit=ISECT_BYTES_PER_CAST,
+                    kernel_bytes_per_unit=round(moved, 2), bytes=agg["drained_casts"] * ISECT_BYTES_PER_CAST,
                     busy_ms=agg["drain_busy_ms"], launches=max(agg["drain_launches_timed"], 1),
                     sum_ms=agg["drain_ms"], casts=agg["drained_casts"],
-                    basis="queued path read once + its film write, per drained path / union of the drain "
-                          "launch intervals (the path's later casts stay in registers)")
+                    basis="SURVEY 8(d) 52 B per ray cast of all drain launches / union of their intervals (the "
+                          "drain keeps a path in registers between casts: it moves kernel_bytes_per_unit per cast)")
         dom_name = max(kernels, key=lambda k: kernels[k]["busy_ms"])
         dom = kernels[dom_name]
         launches = dom["launches"]
@@ -558,9 +562,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": dom_name,
                          "basis": dom["basis"],
-                         "limiter": None if dom["unit"] == "ray cast" else
-                                    "latency of dependent node / triangle gathers and VALU issue (the lane loop keeps "
-                                    "a path in registers: its HBM bytes are the queue read and the film write)",
+                         "limiter": "latency of dependent node / triangle gathers and VALU issue (DESIGN.md §4)",
                          "bytes_per_unit": bytes_per_unit, "kernel_bytes_per_unit": kernel_bytes_per_unit,
                          "unit_of_work": dom["unit"],
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),

@@ -81,7 +81,7 @@ enum {
     SPT_FLAG_FUSED = 4u,           /* one persistent trace+shade kernel per sample chunk */
     SPT_FLAG_WAVEFRONT = 8u,       /* isect / shade / refill kernels over path queues, with the
                                       drain (neither flag: spt_config.pipeline; AUTO = fused iff
-                                      the tile has at most fused_max_paths paths, 0 by default,
+                                      the tile has at most fused_max_paths paths, 2^20 by default,
                                       or at most wavefront_paths when that is set) */
     SPT_FLAG_TIMING_ALL = 16u      /* with SPT_FLAG_TIMING: also shade / refill / resolve launches */
 };
@@ -208,7 +208,7 @@ spt_status spt_scene_create_ex(const int32_t* pos_tri, const float* pos, uint64_
  * SPT_ERR_INVALID for a value outside them.  Build fields are read only by
  * spt_scene_create_cfg; render / intersect fields by every later call. */
 enum {
-    SPT_PIPELINE_AUTO = 0,      /* fused iff W*H*spp of the tile <= fused_max_paths (default 0: never) */
+    SPT_PIPELINE_AUTO = 0,      /* fused iff W*H*spp of the tile <= fused_max_paths (2^20) */
     SPT_PIPELINE_WAVEFRONT = 1, /* isect / shade / refill over path queues */
     SPT_PIPELINE_FUSED = 2      /* one persistent trace+shade kernel per sample chunk */
 };
@@ -233,9 +233,10 @@ typedef struct spt_config {
     uint32_t stack_slack;           /* extra LDS stack entries per lane (0)                  [0..64] */
     /* --- spt_render */
     uint32_t pipeline;              /* SPT_PIPELINE_* (the params' FUSED / WAVEFRONT flags win) [0..2] */
-    uint64_t fused_max_paths;       /* AUTO rule: fused for tiles of <= this many paths, 0 (the
-                                       wavefront with its drain matches or beats the fused kernel
-                                       at every tile size measured: DESIGN.md §6)              */
+    uint64_t fused_max_paths;       /* AUTO rule: fused for jobs of <= this many paths, 2^20 (fewer
+                                       than two chip fills of lanes; from config 1's 1/8 tile up
+                                       the wavefront with its drain matches or beats the fused
+                                       kernel: DESIGN.md §6)                                   */
     uint32_t wavefront_paths;       /* paths in flight when params.wavefront_paths == 0, 2^25 [1..2^31) */
     uint32_t streams;               /* sub-wavefronts (HIP streams) of the wavefront, 4      [1..4] */
     uint32_t isect_refill_idle;     /* refill a wave once this many lanes are idle, 24       [1..64] */

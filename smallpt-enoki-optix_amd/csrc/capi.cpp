@@ -1100,7 +1100,7 @@ void spt_default_config(spt_config* c) {
     c->ploc_radius = 16;
     c->stack_slack = 0;
     c->pipeline = SPT_PIPELINE_AUTO;
-    c->fused_max_paths = 0;
+    c->fused_max_paths = kDefaultFusedMaxPaths;
     c->wavefront_paths = kDefaultWavefrontPaths;
     c->streams = 4;
     c->isect_refill_idle = 24;

@@ -53,6 +53,10 @@ constexpr uint64_t kPixelMajorWavefrontPaths = 24ull << 20;
 // spt_config.drain_q8 default: a sub-wavefront's queue shorter than this many
 // 1/256ths of its persistent isect lanes goes to the drain launch
 constexpr uint32_t kDefaultDrainQ8 = 1024;
+// spt_config.fused_max_paths default: AUTO runs the fused kernel only for jobs
+// of at most 1M paths, fewer than two chip fills of lanes (config 0's 262k:
+// the wavefront's launches and streams outweigh the work, 372 vs 823 Mpaths/s)
+constexpr uint64_t kDefaultFusedMaxPaths = 1ull << 20;
 // spt_config.fit_paths default: jobs of at most 2^27 paths start every path at once
 constexpr uint64_t kDefaultFitPaths = 1ull << 27;
 // spt_config.drain_casts default: the drain runs this many casts after a

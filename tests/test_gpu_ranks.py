@@ -44,9 +44,9 @@ def test_bench_ranks_match_one_rank(tmp_path, n):
     assert rec["n_gpus"] == n and rec["value"] > 0
     assert rec["dist"] == {"backend": "gloo", "world_size": n}
     assert rec["work_check"]["paths_device_counted"] == rec["work_check"]["expected"] == 256 * 128 * 4
-    # AUTO runs the wavefront (with its drain) on every tile; the fused
-    # pipeline is timed beside it on the same tiles, with the same image
-    assert rec["config"]["pipeline"] == "wavefront" and rec["config"]["drain"]["drained_paths_per_step"] > 0
-    leg = rec["fused_leg"]
+    # a tile this small (< 2^20 paths) runs fused (AUTO); the other pipeline
+    # is timed beside it on the same tiles, with the same image
+    assert rec["config"]["pipeline"] == "fused"
+    leg = rec["wavefront_leg"]
     assert leg["value"] > 0 and leg["paths_device_counted"] == 256 * 128 * 4 and leg["image_equal"]
     np.testing.assert_array_equal(np.load(tmp_path / "n.npy"), np.load(tmp_path / "one.npy"))

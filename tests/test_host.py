@@ -160,7 +160,7 @@ def test_config_defaults_and_env_overrides():
     c = sptamd.default_config()
     assert (c.build, c.bvh_width, c.collapse, c.ploc_radius) == (0, 6, 0, 16)
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
-    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 0            # spt.h docs = code
+    assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 20      # spt.h docs = code
     assert (c.drain_q8, c.drain_grid_q8, c.drain_casts) == (1024, 0, 1)
     assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 27, 1)
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
