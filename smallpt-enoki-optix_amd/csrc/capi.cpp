@@ -87,6 +87,7 @@ struct Counters {
     uint32_t exhausted;  // RefillArgs::iter_tag of the refill that started the last work item (0: not yet)
     uint32_t pad[2];
     alignas(128) uint32_t isect_next_b;  // SPT_ISECT_CAMERA: the counter of the launches on queue 1
+    alignas(128) uint32_t xcd_next[8][32];  // the drain / fused kernel's per-XCD work counters (one line each)
 };
 uint32_t* isect_next_of(Counters* c, int queue) { return queue ? &c->isect_next_b : &c->isect_next; }
 
@@ -707,7 +708,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(isect_static_share_q8, 0, 255)
     CFG_RANGE(isect_chunk, 1, 4096)
     CFG_RANGE(isect_grid_q8, 0, 4096)
-    CFG_RANGE(xcd_remap, 0, 3)
+    CFG_RANGE(xcd_remap, 0, 7)
     CFG_RANGE(fused_refill_idle, 1, 64)
     CFG_RANGE(fused_static_share_q8, 0, 255)
     CFG_RANGE(fused_grid_q8, 0, 4096)
@@ -2092,6 +2093,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // the drain: not with traversal counters (isect kernel only) or camera
     // paths started inside the isect launches (an experiment)
     const bool drain_on = cfg.drain_q8 != 0 && !trav_stats && !kIsectCam;
+    // spt_config.xcd_remap bit 2: XCD-aware work distribution in the lane loops (drain, fused)
+    const bool lane_xcd = (cfg.xcd_remap & 4u) != 0;
     // spt_config.drain_sort: a forced drain takes its queue sorted (wide-BVH scenes)
     const bool drain_sort = drain_on && cfg.drain_sort != 0 && sc->nodes8 != nullptr;
     uint64_t drain_launches = 0;
@@ -2143,6 +2146,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         R.mode = mode;
         R.isect_next = &b.cnt->isect_next;
         R.exhausted = &b.cnt->exhausted;
+        R.xcd_next = lane_xcd ? &b.cnt->xcd_next[0][0] : nullptr;
         I.drain_below = 0;
         S.drain_below = 0;
         if (drain_on) {
@@ -2161,6 +2165,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             D.drained = &slot->dev->drained;
             D.drained_casts = &slot->dev->drained_casts;
             D.next = &b.cnt->isect_next;  // zeroed by the refill before; an isect that skips leaves it
+            D.xcd_next = lane_xcd ? &b.cnt->xcd_next[0][0] : nullptr;  // zeroed by the refill before
             D.initstate = p.rng_initstate;
             D.P = (uint32_t)P; D.W = p.width; D.max_depth = p.max_depth;
             D.rr_start = p.rr_start_depth; D.rng_order = p.rng_order;
@@ -2176,7 +2181,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
 
     uint64_t iters = 0;
     if (fused) {
-        FusedArgs F;
+        FusedArgs F{};
         F.sc = sc->dev();
         F.cam = cam;
         F.sample_jump = jumps;
@@ -2185,6 +2190,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         F.sflag = sflag;
         F.stats = slot->dev->stats;
         F.next = &ws.sub[0].cnt->isect_next;
+        F.xcd_next = lane_xcd ? &ws.sub[0].cnt->xcd_next[0][0] : nullptr;
         F.initstate = p.rng_initstate;
         F.P = (uint32_t)P; F.W = p.width; F.max_depth = p.max_depth;
         F.rr_start = p.rr_start_depth; F.rng_order = p.rng_order;
@@ -2206,6 +2212,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             F.pm_ns = pixel_major ? ns : 0;
             HIP_TRY(clear_film(ns));
             HIP_TRY(hipMemsetAsync(F.next, 0, sizeof(uint32_t), stream));
+            if (F.xcd_next) HIP_TRY(hipMemsetAsync(F.xcd_next, 0, sizeof(uint32_t) * 8 * 32, stream));
             if ((st = mark(1, stream, [&] { return launch_fused(F, mode, stream, &lanes); }))) return st;
             if ((st = mark(3, stream, [&] { return resolve(s0, ns); }))) return st;
             iters++;

@@ -1051,6 +1051,8 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         *a.qn_out = surv + total;
         *a.isect_next = 0;
         if (a.surv_clear) *a.surv_clear = 0;
+        if (a.xcd_next)
+            for (uint32_t x = 0; x < 8u; x++) a.xcd_next[x * 32u] = 0;
         if (cur < a.work_end && cur + total >= a.work_end) *a.exhausted = a.iter_tag;
         if (a.casts_in) {  // the shade before: its queue count and its survivors
             const uint32_t casts = *a.casts_in;
@@ -1317,13 +1319,21 @@ void render_fused_kernel(FusedArgs a) {
     float thr = 1.0f, thg = 1.0f, thb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
     bool busy = false, pending = false;
     uint32_t casts = 0, conts = 0, starts = 0;  // wave-uniform
-    // wave-uniform work pool: static share, then dynamic chunks
+    // wave-uniform work pool: static share, then dynamic chunks.  XCD-aware
+    // (a.xcd_next): blocks are dealt round-robin over the 8 XCDs (block b on
+    // XCD b mod 8, MI355X_MICROARCH.md), so the waves of one XCD take adjacent
+    // static shares, and dynamic chunks first from their XCD's eighth of the
+    // rest (its own counter), then from the other XCDs' (stealing): each
+    // XCD's L2 then serves a contiguous range of the work — a band of the
+    // tile in pixel-major order — instead of chunks from all over it.
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
-    const uint32_t wave_id = wave_uniform(blockIdx.x * (kIsectBlock / 64) + (threadIdx.x >> 6));
+    const uint32_t blk = a.xcd_next ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t wave_id = wave_uniform(blk * (kIsectBlock / 64) + (threadIdx.x >> 6));
     const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
     const uint32_t dyn_base = share * nwaves;
     uint32_t pool = wave_id * share, pool_end = pool + share;
     bool drained = false;
+    uint32_t xcd = wave_uniform(blockIdx.x & 7u), xcd_tries = 0;
     while (true) {
         if ((uint32_t)__popcll(__ballot(!busy)) >= a.refill_idle) {
             // ---- shade every pending lane (shade_kernel, main.cpp:404-425)
@@ -1419,7 +1429,24 @@ void render_fused_kernel(FusedArgs a) {
             // ---- new camera paths in free lanes (refill_kernel)
             uint64_t idle = __ballot(!busy && !pending);
             while (idle && !(drained && pool == pool_end)) {
-                if (pool == pool_end) {
+                if (pool == pool_end && a.xcd_next) {
+                    // this XCD's eighth of [dyn_base, n), then the next XCD's
+                    while (xcd_tries < 8u) {
+                        const uint32_t lo = dyn_base + (uint32_t)((uint64_t)(n - dyn_base) * xcd / 8u);
+                        const uint32_t hi = dyn_base + (uint32_t)((uint64_t)(n - dyn_base) * (xcd + 1u) / 8u);
+                        uint32_t got = 0;
+                        if ((threadIdx.x & 63u) == 0) got = atomicAdd(a.xcd_next + xcd * 32u, a.chunk);
+                        got = wave_uniform((uint32_t)__shfl((int)got, 0));
+                        if (got < hi - lo) {
+                            pool = lo + got;
+                            pool_end = min(pool + a.chunk, hi);
+                            break;
+                        }
+                        xcd = (xcd + 1u) & 7u;
+                        xcd_tries++;
+                    }
+                    if (xcd_tries >= 8u) { drained = true; break; }
+                } else if (pool == pool_end) {
                     uint32_t base = 0;
                     if ((threadIdx.x & 63u) == 0) base = atomicAdd(a.next, a.chunk);
                     base = dyn_base + wave_uniform((uint32_t)__shfl((int)base, 0));

@@ -246,6 +246,7 @@ struct RefillArgs {
     uint32_t* qn_out;           // queue count for the next isect, thread 0 only
     uint32_t* isect_next;       // zeroed by thread 0 for the next isect launch
     uint32_t* surv_clear;       // zeroed by thread 0: the next shade's survivor counter (may be null)
+    uint32_t* xcd_next;         // zeroed by thread 0 (8 counters, 32 words apart): the drain's (may be null)
     const uint32_t* casts_in;   // the preceding shade's queue count (null for a chunk's first refill):
                                 // thread 0 adds it and *surv to stats[0] / stats[1]
     const PcgJump* sample_jump; // [spp]: seeded, then s * (4 + 2D) draws on (pcg_seeded_jump)
@@ -364,6 +365,8 @@ struct FusedArgs {
     unsigned long long* drained;    // paths the drain launches took over
     unsigned long long* drained_casts;  // ray casts the drain launches traced
     const uint32_t* perm;           // null, or the order the drain takes queue slots in (launch_drain_sort)
+    uint32_t* xcd_next;             // null, or 8 per-XCD dynamic work counters, 32 words apart (zeroed
+                                    // before the launch): XCD-aware work distribution (spt_config.xcd_remap bit 2)
 };
 
 struct HitInfoArgs {

@@ -72,7 +72,8 @@ def test_drain_bitexact(mesh, mode, q8, casts, streams, wf, monkeypatch):
     # on a side stream: the set's own (CU-masked) streams, fit_streams sub-wavefronts
     # (a caller's null stream gets plain streams and one sub-wavefront for a fitting job)
     side = torch.cuda.Stream()
-    film, st = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, **kw), stream=side)
+    film, st = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, pipeline="wavefront", **kw),
+                        stream=side)
     torch.cuda.synchronize()
     osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
                         sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
@@ -89,7 +90,7 @@ def test_drain_bitexact(mesh, mode, q8, casts, streams, wf, monkeypatch):
         assert st["drained_paths"] > 0 and st["streams"] == streams
     # the same render from the null stream: plain streams, one sub-wavefront when it fits
     if q8 == 1024 and casts == 1 and not wf:
-        film0, st0 = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, **kw))
+        film0, st0 = s.render(sptamd.make_params(W, H, SPP, D, wavefront_paths=wf, pipeline="wavefront", **kw))
         torch.cuda.synchronize()
         np.testing.assert_array_equal(film0.cpu().numpy(), ref)
         assert st0["streams"] == 1
@@ -105,7 +106,7 @@ def test_drain_sorted_bitexact(mesh, mode, monkeypatch):
     s = gpu_scene(mesh, mat, drain_sort=1)
     kw = dict(rr_start_depth=3)
     side = torch.cuda.Stream()
-    film, st = s.render(sptamd.make_params(W, H, SPP, D, **kw), stream=side)
+    film, st = s.render(sptamd.make_params(W, H, SPP, D, pipeline="wavefront", **kw), stream=side)
     torch.cuda.synchronize()
     osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
                         sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
@@ -121,7 +122,7 @@ def test_drain_sample_chunks(mesh, monkeypatch):
     mat = materials(mesh, "albedo")
     s = gpu_scene(mesh, mat, film_budget_bytes=12 * W * H * 2)
     kw = dict(rr_start_depth=2)
-    film, st = s.render(sptamd.make_params(W, H, 7, D, **kw))
+    film, st = s.render(sptamd.make_params(W, H, 7, D, pipeline="wavefront", **kw))
     torch.cuda.synchronize()
     ref, casts = O.OracleScene(mesh, albedo=mat["albedo"]).render(O.reference_params(W, H, 7, D, **kw))
     np.testing.assert_array_equal(film.cpu().numpy(), ref)
