@@ -2385,7 +2385,9 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                     sa[k].count_in = &b.cnt->qn[c];
                     sa[k].count_out = &b.cnt->surv[nx];
                     if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], mode, known[k], strm[k]); }))) return st;
-                    if (dph) {
+                    // (at a chunk's first iteration the count is known exactly: no
+                    // conditional drain when it cannot be short)
+                    if (dph && !(it == 0 && known[k] >= drain_T[k])) {
                         da[k].q = q[k][c];
                         da[k].qcount = &b.cnt->qn[c];
                         da[k].drain_below = drain_T[k];
