@@ -414,11 +414,12 @@ def main():
         # kernel occupies the chip, <= ms_per_step.  `per_launch` keeps the
         # per-launch figure (a 1/K-chip rate when K > 1).  Fused:
         # render_fused_kernel runs the whole path (trace + shade + bounce) in
-        # registers, so its unit is the path and its algorithmic bytes are
-        # what it moves, the per-sample film write (1 B in the reference's
-        # unit mode, 12 B of RGB otherwise); SURVEY §8(d)'s whole-path model
-        # B_path = 84 + 120 S + 60 C (what the wavefront moves for the same
-        # path) is reported beside it as `equivalent_wavefront`.
+        # registers; its unit is the ray cast at SURVEY §8(d)'s 52 B, like the
+        # isect kernel and the drain, while what it moves is the per-sample
+        # film write (1 B in the reference's unit mode, 12 B of RGB
+        # otherwise: kernel_bytes_per_unit); §8(d)'s whole-path model B_path =
+        # 84 + 120 S + 60 C over its busy time is reported beside it as
+        # `equivalent_wavefront`.
         fused = bool(st.get("fused"))
         work_order = {1: "sample-major", 2: "pixel-major"}.get(st.get("work_order"), "?")
         if scene.backend.config["work_order"] == 0:
@@ -442,11 +443,17 @@ def main():
         isect_casts = agg["ray_casts"] - agg["drained_casts"]
         kernels = {}
         if fused:
+            # the same per-cast basis as the drain (the same lane loop): SURVEY
+            # §8(d)'s 52 B per cast; the kernel itself moves only its film writes
+            # (kernel_bytes_per_unit per cast), so the HBM fraction is low and
+            # `limiter` names what bounds it
             kernels["render_fused_kernel"] = dict(
-                units=agg["paths"], unit="path", bytes_per_unit=film_b, kernel_bytes_per_unit=film_b,
-                bytes=agg["paths"] * film_b, busy_ms=agg["isect_busy_ms"], launches=isect_launches,
+                units=agg["ray_casts"], unit="ray cast", bytes_per_unit=ISECT_BYTES_PER_CAST,
+                kernel_bytes_per_unit=round(agg["paths"] * film_b / max(agg["ray_casts"], 1), 3),
+                bytes=agg["ray_casts"] * ISECT_BYTES_PER_CAST, busy_ms=agg["isect_busy_ms"], launches=isect_launches,
                 sum_ms=agg["isect_ms"], casts=agg["ray_casts"],
-                basis="film bytes the fused kernel writes for rank 0's paths / union of its launch intervals")
+                basis="SURVEY 8(d) 52 B per ray cast of all fused launches / union of their intervals (the fused "
+                      "kernel keeps a path in registers: it moves kernel_bytes_per_unit per cast, its film write)")
         else:
             kernels["isect_queue_kernel"] = dict(
                 units=isect_casts, unit="ray cast", bytes_per_unit=ISECT_BYTES_PER_CAST,
@@ -483,7 +490,7 @@ def main():
                 "grays_per_s": round(v["casts"] / (v["busy_ms"] * 1e-3) / 1e9, 4) if v["busy_ms"] > 0 else None}
             for k, v in kernels.items()}
         equiv = None
-        if dom["unit"] != "ray cast":
+        if fused:
             eq_gbs = paths / world * b_path / (busy_ms * 1e-3) / 1e9 if busy_ms > 0 else 0.0
             equiv = {"bytes_per_path": round(b_path, 1), "achieved": round(eq_gbs, 2),
                      "frac": round(eq_gbs / HBM_PEAK_GBS, 5),
