@@ -153,16 +153,20 @@ def cpu_share():
 
 def stream_copy_gbs(torch, dev, nbytes=1 << 30, reps=5):
     """Measured HBM peak for the roofline (BASELINE.md plan): a device-to-device
-    copy of nbytes, read + write bytes over the best of reps (HIP events)."""
+    copy of nbytes through torch's vectorised elementwise kernel (b = a * 1),
+    read + write bytes over the best of reps (HIP events).  That kernel reads
+    6.24 TB/s on the box, the float4-copy rate MI355X_MICROARCH.md quotes
+    (6.29); `copy_` goes through the runtime's blit kernel at 5.2
+    (profiles/r05_exp/c4_knobs_copy/copy_peak.log, tools/copy_peak.py)."""
     a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
     b = torch.empty_like(a)
     a.fill_(1.0)
-    b.copy_(a)
+    torch.mul(a, 1.0, out=b)
     best = None
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        b.copy_(a)
+        torch.mul(a, 1.0, out=b)
         e1.record()
         e1.synchronize()
         ms = e0.elapsed_time(e1)
