@@ -299,10 +299,18 @@ def main():
     # Consecutive steps alternate between two streams and two film buffers
     # (the library alternates two working sets), so a step's render can start
     # while the previous one drains; the gathers stay in step order.
-    # two side streams, not the legacy default stream (whose implicit
-    # synchronisation semantics a caller overlapping work should avoid;
-    # DESIGN.md §6b)
-    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    # two side streams with a hardware queue each (sptamd.queue_stream, as
+    # INTEGRATION.md tells a caller queueing renders): on two ordinary streams
+    # that HIP happened to map onto one hardware queue, the caller-side wait
+    # that ends one render blocked the next render's start, and about one run
+    # in ten lost the overlap (~30 % slower).  SPT_BENCH_STREAMS
+    # =pool: two torch pool streams instead (the earlier behaviour, A/B only).
+    if os.environ.get("SPT_BENCH_STREAMS", "queue") == "pool":
+        streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    elif os.environ.get("SPT_BENCH_STREAMS") == "prio":  # experiment: normal + high priority pool streams
+        streams = [torch.cuda.Stream(device=dev, priority=0), torch.cuda.Stream(device=dev, priority=-1)]
+    else:
+        streams = [sptamd.queue_stream(dev.index if dev.index is not None else 0) for _ in range(2)]
     films = [film, tg.tile_view(1)]
     last_gather = [None]
 

@@ -12,6 +12,7 @@ reference's OPTIX_CHECK / CUDA_CHECK raise std::runtime_error.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import math
 import os
@@ -32,6 +33,57 @@ RAY_TMAX = 1e20
 def _stream_handle(stream: Optional[torch.cuda.Stream]) -> Optional[int]:
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream or None
+
+
+def queue_stream(device: Optional[int] = None) -> torch.cuda.ExternalStream:
+    """A caller stream with a hardware queue of its own, for queued renders.
+
+    HIP maps ordinary streams onto the process's GPU_MAX_HW_QUEUES hardware
+    queues, and a stream's wait on an event blocks the whole queue it sits on.
+    spt_render_async ends by making the caller stream wait for the render, so
+    when the two streams renders alternate on share a queue, the next render's
+    start (an event recorded on the other stream) waits behind that wait and
+    the renders stop overlapping: one run in ten of a tile was ~30 % slow
+    (profiles/r05_exp/caller_queues/).  A stream created with a
+    CU mask gets a dedicated queue (the library's own sub-wavefront streams are
+    made the same way); this one has every CU in its mask.  It is a blocking
+    stream, so work on the legacy null stream waits for it.  Made through the
+    HIP runtime (torch offers no CU-mask stream), wrapped for torch; it is
+    destroyed at interpreter exit, after a device synchronisation, before the
+    runtime's own teardown."""
+    dev = torch.cuda.current_device() if device is None else device
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+    hip = _hip_runtime()
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise _lib.SptError("hipExtStreamCreateWithCUMask", rc, "no stream with a dedicated hardware queue")
+    if not _QUEUE_STREAMS:
+        atexit.register(_destroy_queue_streams)
+    _QUEUE_STREAMS.append((dev, handle.value))
+    return torch.cuda.ExternalStream(handle.value, device=torch.device("cuda", dev))
+
+
+_QUEUE_STREAMS = []
+
+
+def _hip_runtime():
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    return hip
+
+
+def _destroy_queue_streams():
+    hip = _hip_runtime()
+    for dev, h in _QUEUE_STREAMS:
+        with torch.cuda.device(dev):
+            hip.hipStreamSynchronize(h)
+            hip.hipStreamDestroy(h)
+    _QUEUE_STREAMS.clear()
 
 
 def _dev_f32(x, device) -> torch.Tensor:

@@ -127,3 +127,32 @@ def test_drain_sample_chunks(mesh, monkeypatch):
     ref, casts = O.OracleScene(mesh, albedo=mat["albedo"]).render(O.reference_params(W, H, 7, D, **kw))
     np.testing.assert_array_equal(film.cpu().numpy(), ref)
     assert st["ray_casts"] == casts and st["drained_paths"] > 0
+
+
+def test_queued_renders_on_queue_streams(mesh, monkeypatch):
+    """sptamd.queue_stream (the caller streams bench.py queues renders on):
+    renders queued back to back, alternating over two such streams and two
+    films, each equal to the oracle, with a read of each film queued on its
+    stream behind the render (the caller-side join)."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    s = gpu_scene(mesh, {})
+    streams = [sptamd.queue_stream(), sptamd.queue_stream()]
+    assert streams[0].cuda_stream != streams[1].cuda_stream
+    seeds = [0x853C49E6748FEA9B + i for i in range(6)]
+    films = [torch.empty((3, H, W), dtype=torch.float32, device="cuda") for _ in range(2)]
+    copies, tickets = [], []
+    for i, seed in enumerate(seeds):
+        st_ = streams[i % 2]
+        _, t = s.render_async(sptamd.make_params(W, H, SPP, D, rng_initstate=seed), film=films[i % 2], stream=st_)
+        tickets.append(t)
+        with torch.cuda.stream(st_):
+            copies.append(films[i % 2].clone())
+    stats = [s.render_wait(t) for t in tickets]
+    torch.cuda.synchronize()
+    osc = O.OracleScene(mesh)
+    for seed, img, st in zip(seeds, copies, stats):
+        ref, casts = osc.render(O.reference_params(W, H, SPP, D, rng_initstate=seed))
+        np.testing.assert_array_equal(img.cpu().numpy(), ref)
+        assert st["ray_casts"] == casts
+        assert_work_complete(st, H, W, SPP)

@@ -60,6 +60,9 @@ def main():
         run_tiles(args, scene, cfg, kw, W, H, spp, D, env)
 
 
+_QUEUE_STREAMS = []
+
+
 def run_tiles(args, scene, cfg, kw, W, H, spp, D, env):
     import torch
 
@@ -70,10 +73,20 @@ def run_tiles(args, scene, cfg, kw, W, H, spp, D, env):
                                wavefront_paths=args.wavefront, **kw)
         rows = len(sptamd._lib.tile_rows(H, 0, n, args.rows_per_group))
         films = [torch.empty((3, rows, W), dtype=torch.float32, device="cuda") for _ in range(2)]
-        # the two caller streams renders alternate on (bench.py: the current
-        # stream and one more); SPT_SIM_POOL=1: two pool streams, no null stream
-        streams = ([torch.cuda.Stream(), torch.cuda.Stream()] if os.environ.get("SPT_SIM_POOL") == "1"
-                   else [torch.cuda.current_stream(), torch.cuda.Stream()])
+        # the two caller streams renders alternate on, as bench.py: two streams
+        # with a hardware queue each (sptamd.queue_stream, made once);
+        # SPT_SIM_POOL=1: two torch pool streams; SPT_SIM_POOL=0: the current
+        # (legacy null) stream and one pool stream
+        pool = os.environ.get("SPT_SIM_POOL", "2")
+        if pool == "2":
+            if not _QUEUE_STREAMS:
+                _QUEUE_STREAMS.extend([sptamd.queue_stream(), sptamd.queue_stream()])
+            streams = list(_QUEUE_STREAMS)
+        elif pool == "3":  # a normal- and a high-priority pool stream (separate queue pools)
+            streams = [torch.cuda.Stream(priority=0), torch.cuda.Stream(priority=-1)]
+        else:
+            streams = ([torch.cuda.Stream(), torch.cuda.Stream()] if pool == "1"
+                       else [torch.cuda.current_stream(), torch.cuda.Stream()])
         for k in range(2):  # one setup render per stream (working set) before the timed steps, as bench.py
             scene.render_wait(scene.render_async(p, film=films[k], stream=streams[k])[1])
         torch.cuda.synchronize()
