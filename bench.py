@@ -371,7 +371,8 @@ def main():
         elapsed = time.perf_counter() - t0
         agg = {"ray_casts": 0, "iterations": 0, "isect_ms": 0.0, "shade_ms": 0.0, "continuations": 0,
                "regenerations": 0, "camera_ms": 0.0, "resolve_ms": 0.0, "isect_launches": 0, "isect_busy_ms": 0.0,
-               "paths": 0, "drained_paths": 0, "drained_casts": 0, "drain_launches": 0, "drain_ms": 0.0}
+               "paths": 0, "drained_paths": 0, "drained_casts": 0, "drain_launches": 0, "drain_ms": 0.0,
+               "lockstep_casts": 0}
         sts += [scene.render_wait(t) for t in tickets]
         for st in sts:
             check_work(st)
@@ -467,7 +468,13 @@ def main():
                 basis="SURVEY 8(d) 52 B per ray cast of all fused launches / union of their intervals (the fused "
                       "kernel keeps a path in registers: it moves kernel_bytes_per_unit per cast, its film write)")
         else:
-            kernels["isect_queue_kernel"] = dict(
+            # the isect launches: a fitting job's first cast runs in the
+            # one-lane-per-ray kernel (spt_config.lockstep_first), later casts
+            # and other jobs in the persistent one; the name says which ran
+            lock = agg["lockstep_casts"]
+            isect_name = ("isect_lockstep_kernel" if lock == isect_casts else
+                          "isect_queue_kernel" if lock == 0 else "isect_lockstep_kernel+isect_queue_kernel")
+            kernels[isect_name] = dict(
                 units=isect_casts, unit="ray cast", bytes_per_unit=ISECT_BYTES_PER_CAST,
                 kernel_bytes_per_unit=KERNEL_BYTES_PER_CAST, bytes=isect_casts * ISECT_BYTES_PER_CAST,
                 busy_ms=agg["isect_busy_ms"], launches=isect_launches, sum_ms=agg["isect_ms"], casts=isect_casts,

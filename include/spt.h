@@ -145,6 +145,8 @@ typedef struct spt_render_stats {
     uint64_t drain_launches;    /* wavefront: drain launches queued (each runs only if its queue is short) */
     uint64_t drained_casts;     /* wavefront: ray casts the drain launches traced (the rest: isect launches) */
     double drain_ms, drain_busy_ms; /* SPT_FLAG_TIMING: drain launch time summed / the union of its intervals */
+    uint64_t lockstep_casts;    /* wavefront: ray casts traced by the one-lane-per-ray isect launches
+                                   (spt_config.lockstep_first), part of the isect launches' casts */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -308,6 +310,12 @@ typedef struct spt_config {
                                        octant and the origin's Morton code (coherent bounce rays
                                        per wave; wide-BVH scenes); 0: queue order.  The image does
                                        not depend on it                                       [0..1] */
+    uint32_t lockstep_first;        /* 1: the first cast of a job that fits in flight (fit_paths) runs in
+                                       a one-lane-per-ray isect kernel without lane refill: coherent
+                                       camera rays finish together, so the persistent kernel's refill
+                                       only costs (config 1 +10 %); 0: the persistent
+                                       isect kernel for every cast.  The image does not depend on it
+                                                                                               [0..1] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -727,6 +727,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(fit_paths, 0, 1ull << 31)
     CFG_RANGE(sub_queues, 0, 1)
     CFG_RANGE(drain_sort, 0, 1)
+    CFG_RANGE(lockstep_first, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -1127,6 +1128,7 @@ void spt_default_config(spt_config* c) {
     c->fit_paths = kDefaultFitPaths;
     c->sub_queues = 1;
     c->drain_sort = 0;
+    c->lockstep_first = 1;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1903,13 +1905,11 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // fused 2308 vs wavefront 1982 Mpaths/s; whole image: 2353 vs 2825.
     // Traversal counters exist in the wavefront isect kernel only.
     const bool trav_stats = (p.flags & SPT_FLAG_TRAVERSAL_STATS) != 0;
-    // the job-size rule: the fused kernel up to fused_max_paths = 32M paths,
-    // one rank's share of config 1 at N >= 2 (tiles 1/2, 1/4, 1/8: fused 4393,
-    // 4187, 3667 vs wavefront 4220, 3572, 2622 Mpaths/s; config 4's tiles
-    // 1/2-1/8 fused 750-788 vs 684-713); the whole config-1 image, 4577 vs
-    // 4505, is within run-to-run noise, so the north-star wavefront keeps the
-    // single-GPU job (profiles/r02_thr/); an explicit wavefront size moves the
-    // rule with it
+    // the job-size rule: the fused kernel up to fused_max_paths = 2^20 paths
+    // (fewer than two chip fills of lanes, config 0), the wavefront above: with
+    // the drain and the fit rule it carries every tile of config 1 at 1.00-1.05x
+    // the fused kernel; an explicit wavefront size moves the rule
+    // with it
     const uint64_t fused_max = p.wavefront_paths ? p.wavefront_paths : cfg.fused_max_paths;
     bool fused = cfg.pipeline == SPT_PIPELINE_AUTO ? P * p.spp <= fused_max : cfg.pipeline == SPT_PIPELINE_FUSED;
     if (p.flags & SPT_FLAG_FUSED) fused = true;
@@ -2227,6 +2227,11 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         // fork: the sub-wavefront streams start after everything queued so far
         HIP_TRY(hipEventRecord(ws.fork_ev, stream));
         for (int k = 1; k < K; k++) HIP_TRY(hipStreamWaitEvent(strm[k], ws.fork_ev, 0));
+        // spt_config.lockstep_first: the first cast of a fitting job — every
+        // path started by the first refill, the count known exactly and long
+        // enough that the isect and shade run (not the drain) — in the
+        // one-lane-per-ray kernel (launch_isect_lockstep)
+        bool lock0[kMaxStreams] = {};
         uint64_t started[kMaxStreams], sub_begin[kMaxStreams], sub_end[kMaxStreams];  // work items known
                                                                                       // started; the share
         for (int k = 0; k < K; k++) {
@@ -2256,6 +2261,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
             sub_begin[k] = wb;
             sub_end[k] = we;
             started[k] = wb + first;
+            lock0[k] = cfg.lockstep_first && fit && drain_on && !trav_stats && first >= drain_T[k];
             // (SPT_ISECT_CAMERA: the first isect launch starts these paths)
             if (!kIsectCam && (st = mark(0, strm[k], [&] { return launch_refill(ra[k], first, strm[k]); })))
                 return st;
@@ -2374,7 +2380,10 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
                         nlive--;
                         continue;
                     }
+                    const bool lockstep = it == 0 && lock0[k];
+                    if (lockstep) rs.lockstep_casts += known[k];
                     if ((st = mark(1, strm[k], [&] {
+                             if (lockstep) return launch_isect_lockstep(ia[k], known[k], strm[k]);
                              return trav_stats ? launch_isect_queue_stats(ia[k], known[k], strm[k])
                                                : cam ? launch_isect_queue_cam(ia[k], known[k], strm[k])
                                                      : launch_isect_queue(ia[k], known[k], strm[k]);

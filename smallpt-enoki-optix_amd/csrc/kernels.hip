@@ -892,6 +892,39 @@ void isect_queue_kernel(IsectQueueArgs a) {
     }
 }
 
+// The first cast of a job that fits in flight (spt_config.lockstep_first):
+// one lane per queued ray, no lane refill.  Those are the camera rays, and
+// coherent ones (a wave holds one pixel's 64 samples in pixel-major order:
+// 94 % SIMD efficiency on config 1, tools/trav_stats.py), so a wave's lanes
+// finish together and the persistent kernel's machinery — pool atomics,
+// idle-lane ballots, a refill branch whose temporaries sit beside the
+// traversal state — only costs: config 1's camera casts trace at 17.5 Grays/s
+// here against 10.4 in isect_queue_kernel (profiles/r05_exp/lockstep_first/).
+// Later casts are incoherent, where the persistent kernel wins.  The same
+// tracer and hit record as isect_queue_kernel, so the same bits.
+template <typename Tr, bool kNt>
+__global__ __launch_bounds__(kIsectBlock) __attribute__((amdgpu_waves_per_eu(Tr::kMinWaves, 8)))
+void isect_lockstep_kernel(IsectQueueArgs a) {
+    extern __shared__ uint32_t lds_stack[];
+    const Lds L = block_lds(lds_stack);
+    const uint32_t n = *a.count;
+    if (n < a.drain_below) return;  // the drain launch after the shade takes this queue
+    const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
+    if (i >= n) return;
+    const float4 q1 = ldq<kNt>(a.q.q1 + i), q2 = ldq<kNt>(a.q.q2 + i);
+    const uint32_t depth = f2u(q1.w) & ((1u << kMetaDepthBits) - 1u);
+    NoStats st;
+    Tr tr;
+    // any-hit for the last cast unless emitters need the surface (isect_queue_kernel)
+    tr.init(a.sc, v3(q1.x, q1.y, q1.z), v3(q2.x, q2.y, q2.z), kRayTmin, kRayTmax,
+            depth + 1 >= a.max_depth && !a.sc.emission, L);
+    if (!tr.finished())
+        while (!tr.step(a.sc, L, st)) {
+        }
+    const TraceHit hh = tr.hit(a.sc, L);
+    stq<kNt>(a.hits + i, make_float4(u2f((uint32_t)hh.slot), hh.t, hh.u, hh.v));
+}
+
 // __raygen__rg (wavefront_isect.cu:80-112) semantics for the public C ABI.
 // One instance per node format, so each keeps only its own tracer's registers.
 template <typename Tr>
@@ -1741,6 +1774,27 @@ hipError_t launch_isect_queue_cam(const IsectQueueArgs& a, uint32_t grid_items, 
     if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, false, true>(a, grid_items, s);
     return a.sc.node6 ? launch_isect_queue_t<Tracer6, false, true>(a, grid_items, s)
                       : launch_isect_queue_t<Tracer8, false, true>(a, grid_items, s);
+}
+
+template <typename Tr, bool kNt>
+static hipError_t launch_isect_lockstep_t(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+    if (grid_items == 0) return hipSuccess;
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
+    hipLaunchKernelGGL((isect_lockstep_kernel<Tr, kNt>), dim3(blocks_for(grid_items, kIsectBlock)), dim3(kIsectBlock),
+                       lds, s, a);
+    return hipGetLastError();
+}
+
+// grid_items: the queue count, known exactly (a fitting job's first cast)
+hipError_t launch_isect_lockstep(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
+    if (!a.sc.nodes8)
+        return a.nt ? launch_isect_lockstep_t<Tracer, true>(a, grid_items, s)
+                    : launch_isect_lockstep_t<Tracer, false>(a, grid_items, s);
+    if (a.nt)
+        return a.sc.node6 ? launch_isect_lockstep_t<Tracer6, true>(a, grid_items, s)
+                          : launch_isect_lockstep_t<Tracer8, true>(a, grid_items, s);
+    return a.sc.node6 ? launch_isect_lockstep_t<Tracer6, false>(a, grid_items, s)
+                      : launch_isect_lockstep_t<Tracer8, false>(a, grid_items, s);
 }
 
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {

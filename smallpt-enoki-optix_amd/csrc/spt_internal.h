@@ -101,7 +101,7 @@ struct DeviceScene {
     const uint4* nodes8;   // compressed BVH8: 5 per node (bvh_build.h); non-null selects it
     uint32_t node6;        // nodes8 holds 64-B nodes (at most six children, bvh_build.h)
     uint32_t group_shift;  // child s of a node at (group word << group_shift) + s (gpu_bvh8_holes)
-    const float4* tris;    // 3 per slot: v0 (w = original id bits), v1, v2
+    const float4* tris;    // kTriQuads per slot: the rotated-vertex record (tri_record_fill)
     const float4* snrm;    // 3 per slot: n0 (w = material id bits), n1, n2
     const float* tc;       // 6 per slot (u0 v0 u1 v1 u2 v2) or null
     const int32_t* orig2slot;
@@ -437,6 +437,8 @@ SPT_HD void work_pixel(uint32_t q, uint32_t W, uint32_t P, uint32_t B, uint32_t&
 }
 
 hipError_t launch_isect_queue(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
+// one lane per queued ray, no lane refill: a fitting job's first cast (coherent camera rays)
+hipError_t launch_isect_lockstep(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_queue_cam(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s);
 hipError_t launch_isect_public(const IsectPublicArgs& a, hipStream_t s);

@@ -4,7 +4,8 @@ shorter than drain_q8/256 of its isect lanes — or any queue drain_casts casts
 later — is finished by one launch whose lanes continue each path in registers.
 Every combination must give the oracle's bits and the device-counted work:
 threshold only, forced only, both; 1 and 3 sub-wavefronts; jobs that fit in
-flight (fit_paths) and jobs that refill (wavefront_paths set); the
+flight (fit_paths) and jobs that refill (wavefront_paths set); a fitting
+job's first cast in the one-lane-per-ray isect kernel or not; the
 reference's unit mode, albedo + roulette, emitters + smallpt spheres with
 mirror / glass; sample chunks (film_budget_bytes)."""
 import numpy as np
@@ -156,3 +157,25 @@ def test_queued_renders_on_queue_streams(mesh, monkeypatch):
         np.testing.assert_array_equal(img.cpu().numpy(), ref)
         assert st["ray_casts"] == casts
         assert_work_complete(st, H, W, SPP)
+
+
+@pytest.mark.parametrize("mode", ["unit", "emit_spheres"])
+@pytest.mark.parametrize("lockstep", [1, 0])
+def test_lockstep_first_cast_bitexact(mesh, mode, lockstep, monkeypatch):
+    """spt_config.lockstep_first: a fitting job's first cast in the
+    one-lane-per-ray isect kernel (isect_lockstep_kernel); drain_q8 = 1 makes
+    the drain threshold small enough for this image to take that path."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, mode)
+    s = gpu_scene(mesh, mat, drain_q8=1, drain_casts=1, lockstep_first=lockstep)
+    kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
+    film, st = s.render(sptamd.make_params(W, H, SPP, D, pipeline="wavefront", **kw), stream=torch.cuda.Stream())
+    torch.cuda.synchronize()
+    osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
+                        sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
+    ref, casts = osc.render(O.reference_params(W, H, SPP, D, **kw))
+    np.testing.assert_array_equal(film.cpu().numpy(), ref)
+    assert st["ray_casts"] == casts
+    assert_work_complete(st, H, W, SPP)
+    assert st["lockstep_casts"] == (W * H * SPP if lockstep else 0)

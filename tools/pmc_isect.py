@@ -1,7 +1,8 @@
-"""Per-launch and per-cast PMC figures of isect_queue_kernel from rocprofv3
---pmc passes over one bench config.
+"""Per-launch and per-cast PMC figures of the isect launches (isect_queue_kernel,
+isect_lockstep_kernel) or another kernel from rocprofv3 --pmc passes over one
+bench config.
 
-    python tools/pmc_isect.py OUT_JSON KEY BENCH_LOG COUNTER_CSV [COUNTER_CSV ...] [--kernel NAME]
+    python tools/pmc_isect.py OUT_JSON KEY BENCH_LOG COUNTER_CSV [COUNTER_CSV ...] [--kernel REGEX]
 
 Each CSV is one pass (run_counter_collection.csv).  Every counter is averaged
 over the isect dispatches of its pass.  BENCH_LOG holds the bench JSON line of
@@ -21,16 +22,17 @@ import csv
 import gzip
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 
-def passes(paths, kernel="isect_queue"):
+def passes(paths, kernel=r"isect_(queue|lockstep)"):
     per = defaultdict(dict)  # counter -> {dispatch: value}
     for path in paths:
         fh = gzip.open(path, "rt") if path.endswith(".gz") else open(path)  # committed passes are gzipped
         for r in csv.DictReader(fh):
-            if kernel not in r["Kernel_Name"]:
+            if not re.search(kernel, r["Kernel_Name"]):
                 continue
             d = per[r["Counter_Name"]]
             d[(path, r["Dispatch_Id"])] = d.get((path, r["Dispatch_Id"]), 0.0) + float(r["Counter_Value"])
@@ -46,7 +48,7 @@ def bench_line(log):
 
 
 def main(out, key, log, *paths):
-    kernel = "isect_queue"
+    kernel = r"isect_(queue|lockstep)"
     paths = list(paths)
     if "--kernel" in paths:
         i = paths.index("--kernel")
@@ -60,7 +62,7 @@ def main(out, key, log, *paths):
     # kernel and the drain): from the bench line's per-kernel table when it
     # names this kernel (the drain: ray casts and drained paths per launch),
     # else its algorithmic bytes per launch / bytes per unit
-    kt = {k: v for k, v in roof.get("kernels", {}).items() if kernel in k}
+    kt = {k: v for k, v in roof.get("kernels", {}).items() if re.search(kernel, k)}
     cast_per_launch = None
     if kt:
         (kname, kv), = kt.items()

@@ -9,7 +9,7 @@ set -u
 out=${1:-gpurun_out/pmc}
 cfg=${CONFIG:-1}
 pipe=${PIPE:-auto}
-regex=isect_queue
+regex='isect_(queue|lockstep)'
 key=config$cfg
 if [ "$pipe" = fused ]; then regex=render_fused; key=config${cfg}_fused; fi
 # KERNEL=drain: the wavefront's drain (render_fused_kernel<drain>), key "config<N>_drain"
@@ -24,7 +24,7 @@ for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
             "TCC_HIT_sum TCC_MISS_sum" \
             "TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 150 rocprofv3 --pmc $ctrs --kernel-include-regex $regex -d "$out/${key}_p$i" -o run \
+  timeout -s KILL 150 rocprofv3 --pmc $ctrs --kernel-include-regex "$regex" -d "$out/${key}_p$i" -o run \
       --output-format csv -- python bench.py --config "$cfg" --pipeline "$pipe" --steps 1 --warmup 1 \
       --no-cpu-baseline > "$out/${key}_p$i.log" 2>&1
   rc=$?
@@ -32,4 +32,4 @@ for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
   if [ $rc -ne 0 ]; then tail -5 "$out/${key}_p$i.log"; exit $rc; fi
   csvs="$csvs $out/${key}_p$i/run_counter_collection.csv"
 done
-python tools/pmc_isect.py "$out/isect_pmc.json" "$key" "$out/${key}_p1.log" $csvs --kernel $regex
+python tools/pmc_isect.py "$out/isect_pmc.json" "$key" "$out/${key}_p1.log" $csvs --kernel "$regex"

@@ -17,7 +17,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("isect_queue_kernel", "shade_kernel", "refill_kernel", "resolve_flags_kernel", "resolve_kernel",
+    for k in ("isect_queue_kernel", "isect_lockstep_kernel", "shade_kernel", "refill_kernel", "resolve_flags_kernel", "resolve_kernel",
               "render_fused_kernel", "drain_kernel", "fillBuffer", "copyBuffer"):
         if k in name:
             return k
@@ -84,7 +84,7 @@ def main():
         print(f"   queue {q}: {len(lst)} launches, busy {sum(e - s for s, e, *_ in lst) / 1e3:.1f} us, "
               f"gaps {gaps:.1f} us, span {(lst[-1][1] - lst[0][0]) / 1e3:.1f} us")
     print("busy per kernel (summed over queues, us):", {k2: round(v, 1) for k2, v in sorted(busy.items())})
-    iv = [(r[0], r[1]) for r in sel if r[3] == "isect_queue_kernel"]
+    iv = [(r[0], r[1]) for r in sel if r[3] in ("isect_queue_kernel", "isect_lockstep_kernel")]
     print(f"isect union {union(iv) / 1e3:.1f} us; any-kernel union {union([(r[0], r[1]) for r in sel]) / 1e3:.1f} us")
 
 
