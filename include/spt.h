@@ -316,6 +316,12 @@ typedef struct spt_config {
                                        only costs (config 1 +10 %); 0: the persistent
                                        isect kernel for every cast.  The image does not depend on it
                                                                                                [0..1] */
+    uint32_t fit_chunks;            /* 1: a job of more than fit_paths paths whose tile has at most
+                                       fit_paths pixels runs as sample chunks of at most fit_paths
+                                       paths, each started at once like a fitting job (config 3
+                                       +8 %); 0: such jobs keep the per-cast
+                                       wavefront with wavefront_paths in flight.  The image does not
+                                       depend on it                                           [0..1] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

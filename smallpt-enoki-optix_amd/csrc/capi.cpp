@@ -728,6 +728,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(sub_queues, 0, 1)
     CFG_RANGE(drain_sort, 0, 1)
     CFG_RANGE(lockstep_first, 0, 1)
+    CFG_RANGE(fit_chunks, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -1129,6 +1130,7 @@ void spt_default_config(spt_config* c) {
     c->sub_queues = 1;
     c->drain_sort = 0;
     c->lockstep_first = 1;
+    c->fit_chunks = 1;
 }
 
 spt_status spt_scene_set_config(spt_scene sc, const spt_config* cfg) {
@@ -1923,8 +1925,28 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // XCD's L2 on a tile of <= 4M pixels, with 24M paths in flight unless
     // set (config 1 +5.5 %); sample-major otherwise (config 3's 16.7M-pixel
     // tile -2.1 %, smallpt's cache-resident scene -4.6 %).
+    // A job that fits in flight (spt_config.fit_paths): every path starts in
+    // the first refill on fit_streams sub-wavefronts, so its last work item
+    // starts at once and the drain finishes it drain_casts casts later.  The
+    // per-cast launches then run only while the whole job is in flight, and
+    // a render is a handful of launches, which two renders queued on two
+    // streams overlap without sub-wavefront streams of their own (DESIGN.md §6:
+    // stable at the box's four hardware queues, where four sub-wavefront
+    // streams per working set could share a queue with the other set's).
+    // A larger job runs as sample chunks that each fit (spt_config.fit_chunks:
+    // config 3 +8 %, config 2 +0.9 %, profiles/r05_exp/fit_chunks/).
+    // (an explicit paths-in-flight count, in the params or the config, wins)
+    const bool fit_ok = !fused && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths && cfg.fit_paths &&
+                        cfg.drain_q8;
+    uint32_t fit_chunk = 0;  // samples per chunk of a job run as fitting chunks
+    if (fit_ok && P * p.spp > cfg.fit_paths && cfg.fit_chunks && P <= cfg.fit_paths)
+        fit_chunk = (uint32_t)std::min<uint64_t>(p.spp, cfg.fit_paths / P);
+    const bool fit = fit_ok && (P * p.spp <= cfg.fit_paths || fit_chunk != 0);
     const uint64_t scene_bytes = sc->stats.device_bytes;
-    const bool wave_pm = !fused && scene_bytes >= kPixelMajorMinWaveSceneBytes && P <= kPixelMajorMaxWaveTilePx;
+    // (a fitting job of any tile size: pixel-major over scenes beyond an
+    // XCD's L2 — config 3's 16.7M-pixel chunks +8 % with it, its per-cast
+    // wavefront -2.1 %; smallpt's cache-resident scene -4 % either way)
+    const bool wave_pm = !fused && scene_bytes >= kPixelMajorMinWaveSceneBytes && (P <= kPixelMajorMaxWaveTilePx || fit);
     const uint32_t pixel_major =
         cfg.work_order == SPT_WORK_PIXEL_MAJOR ||
         (cfg.work_order == SPT_WORK_AUTO && (scene_bytes >= kPixelMajorMinSceneBytes ||
@@ -1939,18 +1961,7 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
         (cfg.queue_cache == SPT_QUEUE_CACHE_AUTO && scene_bytes >= kPixelMajorMinSceneBytes);
     if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
         C = kPixelMajorWavefrontPaths;
-    // A job that fits in flight (spt_config.fit_paths): every path starts in
-    // the first refill on fit_streams sub-wavefronts, so its last work item
-    // starts at once and the drain finishes it drain_casts casts later.  The
-    // per-cast launches then run only while the whole job is in flight, and
-    // a render is a handful of launches, which two renders queued on two
-    // streams overlap without sub-wavefront streams of their own (DESIGN.md §6:
-    // stable at the box's four hardware queues, where four sub-wavefront
-    // streams per working set could share a queue with the other set's).
-    // (an explicit paths-in-flight count, in the params or the config, wins)
-    const bool fit = !fused && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths && cfg.fit_paths &&
-                     cfg.drain_q8 && P * p.spp <= cfg.fit_paths;
-    if (fit) C = P * p.spp;
+    if (fit) C = fit_chunk ? (uint64_t)fit_chunk * P : P * p.spp;
     C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);
@@ -1983,8 +1994,9 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // running sum in acc.  (A chunk's work items are counted in 32 bits: at
     // most 2^31 per chunk.)
     const uint64_t budget = cfg.film_budget_bytes;
-    const uint32_t chunk = (uint32_t)std::max<uint64_t>(
+    uint32_t chunk = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
+    if (fit_chunk) chunk = std::min(chunk, fit_chunk);  // each chunk fits in flight
     rs.paths_in_flight = (uint32_t)C;
     WorkSet& ws = sc->ws.pick_set(caller);
     ws.last_ticket = sc->ws.next_ticket;

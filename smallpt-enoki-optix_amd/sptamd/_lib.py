@@ -124,7 +124,7 @@ class Config(ctypes.Structure):
                 ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32),
                 ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32),
                 ("fit_streams", c_uint32), ("fit_paths", c_uint64), ("sub_queues", c_uint32),
-                ("drain_sort", c_uint32), ("lockstep_first", c_uint32)]
+                ("drain_sort", c_uint32), ("lockstep_first", c_uint32), ("fit_chunks", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -256,6 +256,7 @@ _ENV_CONFIG = {
     "SPT_SUB_QUEUES": ("sub_queues", int),
     "SPT_DRAIN_SORT": ("drain_sort", int),
     "SPT_LOCKSTEP_FIRST": ("lockstep_first", int),
+    "SPT_FIT_CHUNKS": ("fit_chunks", int),
 }
 
 

@@ -179,3 +179,31 @@ def test_lockstep_first_cast_bitexact(mesh, mode, lockstep, monkeypatch):
     assert st["ray_casts"] == casts
     assert_work_complete(st, H, W, SPP)
     assert st["lockstep_casts"] == (W * H * SPP if lockstep else 0)
+
+
+@pytest.mark.parametrize("mode", ["unit", "albedo", "emit_spheres"])
+@pytest.mark.parametrize("chunks", [1, 0])
+def test_fit_chunks_bitexact(mesh, mode, chunks, monkeypatch):
+    """spt_config.fit_chunks: a job of more than fit_paths paths runs as sample
+    chunks that each start every path at once (2 samples per chunk here, the
+    last chunk short), with the first cast in lockstep; 0: the per-cast
+    wavefront.  Same bits either way."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, mode)
+    s = gpu_scene(mesh, mat, drain_q8=1, drain_casts=1, fit_paths=W * H * 2, fit_chunks=chunks)
+    kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
+    spp = 7
+    film, st = s.render(sptamd.make_params(W, H, spp, D, pipeline="wavefront", **kw), stream=torch.cuda.Stream())
+    torch.cuda.synchronize()
+    osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
+                        sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
+    ref, casts = osc.render(O.reference_params(W, H, spp, D, **kw))
+    np.testing.assert_array_equal(film.cpu().numpy(), ref)
+    assert st["ray_casts"] == casts
+    assert_work_complete(st, H, W, spp)
+    if chunks:
+        assert st["paths_in_flight"] == W * H * 2 and st["lockstep_casts"] == W * H * spp
+        assert st["drained_paths"] > 0
+    else:
+        assert st["lockstep_casts"] == 0

@@ -163,7 +163,7 @@ def test_config_defaults_and_env_overrides():
     assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 20      # spt.h docs = code
     assert (c.drain_q8, c.drain_grid_q8, c.drain_casts) == (1024, 0, 1)
     assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 27, 1)
-    assert (c.drain_sort, c.lockstep_first) == (0, 1)
+    assert (c.drain_sort, c.lockstep_first, c.fit_chunks) == (0, 1, 1)
     assert sptamd.config_from_env(environ={"SPT_LOCKSTEP_FIRST": "0"}).lockstep_first == 0
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
     assert (d.drain_q8, d.drain_casts, d.fit_paths) == (0, 4, 0)
@@ -183,7 +183,7 @@ def test_config_defaults_and_env_overrides():
                                          ("bvh_width", 7), ("pack_groups", 3), ("work_order", 3),
                                          ("queue_cache", 3), ("drain_q8", 65536), ("drain_grid_q8", 4097),
                                          ("drain_casts", 65), ("fit_streams", 0), ("fit_streams", 5),
-                                         ("fit_paths", (1 << 31) + 1), ("lockstep_first", 2)])
+                                         ("fit_paths", (1 << 31) + 1), ("lockstep_first", 2), ("fit_chunks", 2)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)
