@@ -203,7 +203,10 @@ def test_fit_chunks_bitexact(mesh, mode, chunks, monkeypatch):
     assert st["ray_casts"] == casts
     assert_work_complete(st, H, W, spp)
     if chunks:
-        assert st["paths_in_flight"] == W * H * 2 and st["lockstep_casts"] == W * H * spp
+        # every chunk whose queue is not already short goes through the lockstep
+        # first cast (the 1-sample last chunk may be shorter than the drain's
+        # threshold, which depends on the chip's lane count)
+        assert st["paths_in_flight"] == W * H * 2 and W * H * 2 <= st["lockstep_casts"] <= W * H * spp
         assert st["drained_paths"] > 0
     else:
         assert st["lockstep_casts"] == 0
