@@ -559,14 +559,15 @@ def main():
                            "rule": "every step, every rank: paths started == paths ended == tile px x spp, "
                                    "0 film slots unwritten (spt_render_stats)"},
             "dist": {"backend": dist.get_backend() if world > 1 else None, "world_size": world},
-            "work_order_rule": "auto: pixel-major for scenes of >= 256 MiB, fused tiles of >= 16M paths and "
-                               "wavefront tiles of <= 4M px over scenes of >= 4 MiB (24M paths in flight), "
+            "work_order_rule": "auto: pixel-major for scenes of >= 256 MiB, fused tiles of >= 16M paths, and "
+                               "wavefront tiles of <= 4M px or jobs started at once (fit) over scenes of >= 4 MiB, "
                                "else sample-major (DESIGN.md §4)",
             "queue_cache_rule": "auto: non-temporal path-queue / hit accesses for scenes of >= 256 MiB, else "
                                 "cached (DESIGN.md §4)",
             "pipeline_rule": "auto: the wavefront (isect + ballot-compaction shade per cast; a job of <= 2^27 "
-                             "paths starts every path at once on one sub-wavefront and the drain finishes the "
-                             "paths still in flight after drain_casts casts; DESIGN.md §4, §6)"
+                             "paths starts every path at once on two sub-wavefronts, a larger one in sample chunks "
+                             "that each do; the first cast in the one-lane-per-ray isect kernel; the drain finishes "
+                             "the paths still in flight after drain_casts casts; DESIGN.md §4, §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
                        "drain": None if fused else {
