@@ -564,7 +564,7 @@ def main():
                                "else sample-major (DESIGN.md §4)",
             "queue_cache_rule": "auto: non-temporal path-queue / hit accesses for scenes of >= 256 MiB, else "
                                 "cached (DESIGN.md §4)",
-            "pipeline_rule": "auto: the wavefront (isect + ballot-compaction shade per cast; a job of <= 2^27 "
+            "pipeline_rule": "auto: the wavefront (isect + ballot-compaction shade per cast; a job of <= 2^28 "
                              "paths starts every path at once on two sub-wavefronts, a larger one in sample chunks "
                              "that each do; the first cast in the one-lane-per-ray isect kernel; the drain finishes "
                              "the paths still in flight after drain_casts casts; DESIGN.md §4, §6)"

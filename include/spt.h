@@ -298,8 +298,9 @@ typedef struct spt_config {
                                        path in the first refill (paths in flight = the job, unless
                                        params.wavefront_paths or config.wavefront_paths is set) on fit_streams
                                        sub-wavefronts: its last work item starts at once, so the
-                                       drain takes over drain_casts casts later; 2^27 (about 11 GB
-                                       of queues at most), 0: off               */
+                                       drain takes over drain_casts casts later; 2^28 (21 GB of
+                                       queues per working set in unit mode, 34 GB with emitters),
+                                       0: off                                   */
     uint32_t sub_queues;            /* 1: a render runs on its working set's own streams, created
                                        with a full CU mask, which gives each a hardware queue of
                                        its own whatever GPU_MAX_HW_QUEUES allows; they are blocking

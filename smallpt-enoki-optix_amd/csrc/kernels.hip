@@ -89,6 +89,11 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #ifndef SPT_DRAIN_WAVES
 #define SPT_DRAIN_WAVES 7
 #endif
+// the albedo / emitter drains at 6 (80 VGPRs, 48 B of scratch) instead of the
+// fused kernel's 5 (96, 32 B): config 2 +1.7 % (profiles/r05_exp/fit_paths_rgb_waves/)
+#ifndef SPT_DRAIN_WAVES_RGB
+#define SPT_DRAIN_WAVES_RGB 6
+#endif
 #ifndef SPT_DRAIN_WAVES_NT
 #define SPT_DRAIN_WAVES_NT 6
 #endif
@@ -1329,7 +1334,7 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
 template <typename Tr, int kMode, bool kDrain = false, bool kNt = false>
 __global__ __launch_bounds__(kIsectBlock)
 __attribute__((amdgpu_waves_per_eu(kDrain && kMode == kModeUnit ? (kNt ? SPT_DRAIN_WAVES_NT : SPT_DRAIN_WAVES)
-                                                                  : SPT_FUSED_WAVES, 8)))
+                                   : kDrain ? SPT_DRAIN_WAVES_RGB : SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
     extern __shared__ uint32_t lds_stack[];

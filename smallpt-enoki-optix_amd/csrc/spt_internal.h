@@ -57,8 +57,11 @@ constexpr uint32_t kDefaultDrainQ8 = 1024;
 // of at most 1M paths, fewer than two chip fills of lanes (config 0's 262k:
 // the wavefront's launches and streams outweigh the work, 372 vs 823 Mpaths/s)
 constexpr uint64_t kDefaultFusedMaxPaths = 1ull << 20;
-// spt_config.fit_paths default: jobs of at most 2^27 paths start every path at once
-constexpr uint64_t kDefaultFitPaths = 1ull << 27;
+// spt_config.fit_paths default: jobs (or sample chunks, fit_chunks) of at most
+// 2^28 paths start every path at once: 21 GB of queues per working set in unit
+// mode, 34 GB with emitters (HBM is 288 GB); config 3 +3.7 % over 2^27, config
+// 2 -0.7 % (profiles/r05_exp/fit_paths_rgb_waves/)
+constexpr uint64_t kDefaultFitPaths = 1ull << 28;
 // spt_config.drain_casts default: the drain runs this many casts after a
 // sub-wavefront's last work item started, whatever its queue holds
 constexpr uint32_t kDefaultDrainCasts = 1;

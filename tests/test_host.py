@@ -162,7 +162,7 @@ def test_config_defaults_and_env_overrides():
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
     assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 20      # spt.h docs = code
     assert (c.drain_q8, c.drain_grid_q8, c.drain_casts) == (1024, 0, 1)
-    assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 27, 1)
+    assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 28, 1)
     assert (c.drain_sort, c.lockstep_first, c.fit_chunks) == (0, 1, 1)
     assert sptamd.config_from_env(environ={"SPT_LOCKSTEP_FIRST": "0"}).lockstep_first == 0
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
