@@ -89,8 +89,15 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #ifndef SPT_DRAIN_WAVES
 #define SPT_DRAIN_WAVES 7
 #endif
-// the albedo / emitter drains at 6 (80 VGPRs, 48 B of scratch) instead of the
-// fused kernel's 5 (96, 32 B): config 2 +1.7 % (profiles/r05_exp/fit_paths_rgb_waves/)
+// the albedo / emitter drains at 6 (80 VGPRs, 32 B of scratch with the path's
+// throughput and radiance parked in LDS, SPT_PARK_PATH) instead of the fused
+// kernel's 5: config 2 +1.7 % (profiles/r05_exp/fit_paths_rgb_waves/), parking
+// +2.5 % more (profiles/r05_exp/park_path/); 7 waves (64 B of scratch) no better
+// albedo / emitter lane loops keep a path's throughput and radiance in LDS
+// while its ray traces (render_fused_kernel)
+#ifndef SPT_PARK_PATH
+#define SPT_PARK_PATH 1
+#endif
 #ifndef SPT_DRAIN_WAVES_RGB
 #define SPT_DRAIN_WAVES_RGB 6
 #endif
@@ -1355,6 +1362,13 @@ void render_fused_kernel(FusedArgs a) {
     // throughput only (VGPRs: occupancy).
     uint32_t pix = 0, meta = 0;  // tile pixel; sample << 8 | cast (as a queue path's q1.w)
     float thr = 1.0f, thg = 1.0f, thb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
+    // albedo / emitter modes: a lane's throughput and gathered radiance wait in
+    // LDS while its ray traces (two float4 per lane after the tracer's records),
+    // so the traversal loop does not hold them in VGPRs
+    constexpr bool kPark = kMode != kModeUnit && SPT_PARK_PATH;
+    float4* const park = kPark ? (float4*)((char*)L.base + a.sc.stack_depth * kIsectBlock * 4u + Tr::kExtraLds) +
+                                     2u * threadIdx.x
+                               : nullptr;
     bool busy = false, pending = false;
     uint32_t casts = 0, conts = 0, starts = 0;  // wave-uniform
     // wave-uniform work pool: static share, then dynamic chunks.  XCD-aware
@@ -1380,6 +1394,10 @@ void render_fused_kernel(FusedArgs a) {
             if (pending) {
                 pending = false;
                 bool term = true;
+                if constexpr (kPark) {
+                    const float4 p0 = park[0], p1 = park[1];
+                    thr = p0.x; thg = p0.y; thb = p0.z; lr = p0.w; lg = p1.x; lb = p1.y;
+                }
                 const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u), sample = meta >> kMetaDepthBits;
                 TraceHit hh = tr.hit(a.sc, L);
                 if (kMode != kModeUnit && a.sc.nsph)  // smallpt's spheres after the BVH
@@ -1445,6 +1463,10 @@ void render_fused_kernel(FusedArgs a) {
                                 thr = thr * wgt; thg = thg * wgt; thb = thb * wgt;
                             }
                             meta++;  // the next cast
+                            if constexpr (kPark) {
+                                park[0] = make_float4(thr, thg, thb, lr);
+                                park[1] = make_float4(lg, lb, 0.0f, 0.0f);
+                            }
                             tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 2 >= a.max_depth && !kEmit, L);
                             busy = true;
                             cont = true;
@@ -1514,6 +1536,10 @@ void render_fused_kernel(FusedArgs a) {
                         const float2 l = ldq2<kNt>(a.q.rad + j);
                         lg = l.x; lb = l.y;
                     }
+                    if constexpr (kPark) {
+                        park[0] = make_float4(thr, thg, thb, lr);
+                        park[1] = make_float4(lg, lb, 0.0f, 0.0f);
+                    }
                     tr.init(a.sc, v3(q1.x, q1.y, q1.z), dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit, L);
                     busy = true;
                     if (tr.finished()) {  // empty scene: a miss
@@ -1532,6 +1558,10 @@ void render_fused_kernel(FusedArgs a) {
                     meta = sample << kMetaDepthBits;  // cast 0
                     thr = thg = thb = 1.0f;                        // main.cpp:391
                     lr = lg = lb = 0.0f;
+                    if constexpr (kPark) {
+                        park[0] = make_float4(thr, thg, thb, lr);
+                        park[1] = make_float4(lg, lb, 0.0f, 0.0f);
+                    }
                     tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit, L);
                     busy = true;
                     if (tr.finished()) {  // empty scene: a miss
@@ -1878,7 +1908,9 @@ static hipError_t launch_fused_t(const FusedArgs& a, hipStream_t s, uint32_t* la
     static thread_local size_t cached_lds = 0;
     static thread_local uint32_t cached = 0;
     static thread_local int cached_dev = -1;
-    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
+    // + the parked throughput / radiance of albedo / emitter lanes (render_fused_kernel)
+    const size_t park = kMode != kModeUnit && SPT_PARK_PATH ? (size_t)kIsectBlock * 32 : 0;
+    const size_t lds = (size_t)a.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds + park;
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (!cached || cached_lds != lds || cached_dev != dev) {
