@@ -5,8 +5,11 @@ import re
 import subprocess
 import sys
 
-cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Icsrc",
-       "-fhip-fp32-correctly-rounded-divide-sqrt", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
+# the Makefile's device flags (COMMON + HIPFLAGS): without -ffp-contract=off the
+# compiler forms FMAs the product does not, and the register counts differ
+cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-I../include",
+       "-Icsrc", "-x", "hip", "-fhip-fp32-correctly-rounded-divide-sqrt",
+       "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops",
        "-Rpass-analysis=kernel-resource-usage",
        "-c", "csrc/kernels.hip", "-o", "/dev/null"] + sys.argv[1:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
