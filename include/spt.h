@@ -147,6 +147,8 @@ typedef struct spt_render_stats {
     double drain_ms, drain_busy_ms; /* SPT_FLAG_TIMING: drain launch time summed / the union of its intervals */
     uint64_t lockstep_casts;    /* wavefront: ray casts traced by the one-lane-per-ray isect launches
                                    (spt_config.lockstep_first), part of the isect launches' casts */
+    uint64_t fit_paths;         /* the fit size in effect: spt_config.fit_paths, or fewer when the
+                                   queues would not fit in device memory (spt_config.fit_bytes) */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -323,6 +325,13 @@ typedef struct spt_config {
                                        +8 %); 0: such jobs keep the per-cast
                                        wavefront with wavefront_paths in flight.  The image does not
                                        depend on it                                           [0..1] */
+    uint64_t fit_bytes;             /* device memory a fitting job's path queues and hit records may
+                                       take per working set (2 x 16 B x planes + 16 B per path);
+                                       fit_paths shrinks to what fits (more sample chunks; below
+                                       one chunk of the tile's pixels the per-cast wavefront).
+                                       0: the free device memory plus what the caller's set holds,
+                                       less 1/16 (processes or scenes sharing the GPU).  The image
+                                       does not depend on it                                   */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

@@ -239,6 +239,12 @@ struct Workspace {
     // set on another caller stream can put two of the four sub-wavefronts on
     // one queue, which serialises them (config 3 / 4: -17 % / -16 %,
     // profiles/r03_queues/).
+    // the set bound to caller stream s, if any (pick_set without binding one)
+    const WorkSet* bound_set(hipStream_t s) const {
+        for (const WorkSet& w : sets)
+            if (w.bound && w.home == s) return &w;
+        return nullptr;
+    }
     WorkSet& pick_set(hipStream_t s) {
         WorkSet* lru = &sets[0];
         for (WorkSet& w : sets)
@@ -1936,12 +1942,41 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // A larger job runs as sample chunks that each fit (spt_config.fit_chunks:
     // config 3 +8 %, config 2 +0.9 %, profiles/r05_exp/fit_chunks/).
     // (an explicit paths-in-flight count, in the params or the config, wins)
-    const bool fit_ok = !fused && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths && cfg.fit_paths &&
+    // What a path carries (spt_internal.h PathMode): the reference's case
+    // (every albedo 1, no emitters) needs only the ray and an escaped flag.
+    const bool unit = sc->albedo_unit && sc->ntex == 0 && sc->nsph == 0 && sc->nkind == 0;
+    const int mode = sc->emission ? kModeEmit : (unit ? kModeUnit : kModeAlbedo);
+    const uint64_t film_unit = mode_film_bytes(mode);
+    // A fitting job's queues and hit records must fit in device memory
+    // (spt_config.fit_bytes; 0: the free memory plus what this caller's set
+    // holds, less 1/16 — processes or scenes sharing the GPU): fit_paths
+    // shrinks to what fits, into more sample chunks, and below one chunk of
+    // the tile's pixels the job keeps the per-cast wavefront.  Asked only when
+    // the set must grow.
+    uint64_t fit_paths = cfg.fit_paths;
+    if (fit_paths && !fused) {
+        const uint64_t per_path = 2ull * 16 * mode_planes(mode) + kHitBytes;
+        const uint64_t want = std::min<uint64_t>(fit_paths, P * p.spp) * per_path;
+        uint64_t held = 0;
+        if (const WorkSet* hs = sc->ws.bound_set(caller))
+            for (const Sub& b : hs->sub) held += (uint64_t)b.cap * (2ull * 16 * b.planes + kHitBytes);
+        uint64_t room = cfg.fit_bytes;
+        if (!room && want > held) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+                room = held + fr - fr / 16;
+            else
+                (void)hipGetLastError();
+        }
+        if (room && want > room) fit_paths = room / per_path;
+    }
+    rs.fit_paths = fit_paths;
+    const bool fit_ok = !fused && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths && fit_paths &&
                         cfg.drain_q8;
     uint32_t fit_chunk = 0;  // samples per chunk of a job run as fitting chunks
-    if (fit_ok && P * p.spp > cfg.fit_paths && cfg.fit_chunks && P <= cfg.fit_paths)
-        fit_chunk = (uint32_t)std::min<uint64_t>(p.spp, cfg.fit_paths / P);
-    const bool fit = fit_ok && (P * p.spp <= cfg.fit_paths || fit_chunk != 0);
+    if (fit_ok && P * p.spp > fit_paths && cfg.fit_chunks && P <= fit_paths)
+        fit_chunk = (uint32_t)std::min<uint64_t>(p.spp, fit_paths / P);
+    const bool fit = fit_ok && (P * p.spp <= fit_paths || fit_chunk != 0);
     const uint64_t scene_bytes = sc->stats.device_bytes;
     // (a fitting job of any tile size: pixel-major over scenes beyond an
     // XCD's L2 — config 3's 16.7M-pixel chunks +8 % with it, its per-cast
@@ -1984,11 +2019,6 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
     const uint64_t Ck = (C + K - 1) / K;
-    // What a path carries (spt_internal.h PathMode): the reference's case
-    // (every albedo 1, no emitters) needs only the ray and an escaped flag.
-    const bool unit = sc->albedo_unit && sc->ntex == 0 && sc->nsph == 0 && sc->nkind == 0;
-    const int mode = sc->emission ? kModeEmit : (unit ? kModeUnit : kModeAlbedo);
-    const uint64_t film_unit = mode_film_bytes(mode);
     // Per-sample contribution film [chunk][P] bytes (unit) or [chunk][3][P]
     // floats, at most film_budget_bytes (4 GiB) per chunk; chunks carry the
     // running sum in acc.  (A chunk's work items are counted in 32 bits: at

@@ -95,7 +95,8 @@ class RenderStats(ctypes.Structure):
                 ("isect_tri_wave_steps", c_uint64), ("isect_node_wave_steps", c_uint64),
                 ("isect_begin_ms", c_double), ("isect_end_ms", c_double),
                 ("drained_paths", c_uint64), ("drain_launches", c_uint64), ("drained_casts", c_uint64),
-                ("drain_ms", c_double), ("drain_busy_ms", c_double), ("lockstep_casts", c_uint64)]
+                ("drain_ms", c_double), ("drain_busy_ms", c_double), ("lockstep_casts", c_uint64),
+                ("fit_paths", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -124,7 +125,8 @@ class Config(ctypes.Structure):
                 ("pixel_block", c_uint32), ("work_order", c_uint32), ("queue_cache", c_uint32),
                 ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32),
                 ("fit_streams", c_uint32), ("fit_paths", c_uint64), ("sub_queues", c_uint32),
-                ("drain_sort", c_uint32), ("lockstep_first", c_uint32), ("fit_chunks", c_uint32)]
+                ("drain_sort", c_uint32), ("lockstep_first", c_uint32), ("fit_chunks", c_uint32),
+                ("fit_bytes", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -257,6 +259,7 @@ _ENV_CONFIG = {
     "SPT_DRAIN_SORT": ("drain_sort", int),
     "SPT_LOCKSTEP_FIRST": ("lockstep_first", int),
     "SPT_FIT_CHUNKS": ("fit_chunks", int),
+    "SPT_FIT_BYTES": ("fit_bytes", int),
 }
 
 

@@ -210,3 +210,36 @@ def test_fit_chunks_bitexact(mesh, mode, chunks, monkeypatch):
         assert st["drained_paths"] > 0
     else:
         assert st["lockstep_casts"] == 0
+
+
+@pytest.mark.parametrize("mode", ["unit", "emit_spheres"])
+def test_fit_bytes_shrinks_fit(mesh, mode, monkeypatch):
+    """spt_config.fit_bytes: a fitting job whose queues and hit records would
+    exceed it runs with fit_paths cut to what fits (here 2 of 5 samples' paths
+    per chunk), and with less than one chunk of the tile's pixels on the
+    per-cast wavefront.  fit_bytes 0 asks the device for its free memory (the
+    default, a full fit here).  Same bits every way."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, mode)
+    planes = 2 if mode == "unit" else 4
+    per_path = 2 * 16 * planes + 16  # two queues of `planes` 16-B planes + the hit record
+    kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
+    spp = 5
+    osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
+                        sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
+    ref, casts = osc.render(O.reference_params(W, H, spp, D, **kw))
+    for fit_bytes, fit_paths, in_flight in [(0, 1 << 28, W * H * spp),
+                                            (W * H * 2 * per_path + 10, W * H * 2, W * H * 2),
+                                            (W * H * per_path // 2, W * H // 2, None)]:
+        s = gpu_scene(mesh, mat, drain_q8=1, drain_casts=1, fit_bytes=fit_bytes)
+        film, st = s.render(sptamd.make_params(W, H, spp, D, pipeline="wavefront", **kw), stream=torch.cuda.Stream())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(film.cpu().numpy(), ref)
+        assert st["ray_casts"] == casts
+        assert_work_complete(st, H, W, spp)
+        assert st["fit_paths"] == fit_paths, (fit_bytes, st["fit_paths"])
+        if in_flight is not None:  # fitting (chunks): every chunk's paths in flight, first cast in lockstep
+            assert st["paths_in_flight"] == in_flight and st["lockstep_casts"] > 0
+        else:  # below one chunk of the tile's pixels: the per-cast wavefront, no lockstep cast
+            assert st["lockstep_casts"] == 0

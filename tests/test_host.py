@@ -165,6 +165,7 @@ def test_config_defaults_and_env_overrides():
     assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 28, 1)
     assert (c.drain_sort, c.lockstep_first, c.fit_chunks) == (0, 1, 1)
     assert sptamd.config_from_env(environ={"SPT_LOCKSTEP_FIRST": "0"}).lockstep_first == 0
+    assert c.fit_bytes == 0 and sptamd.config_from_env(environ={"SPT_FIT_BYTES": "4096"}).fit_bytes == 4096
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
     assert (d.drain_q8, d.drain_casts, d.fit_paths) == (0, 4, 0)
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
