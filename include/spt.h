@@ -325,13 +325,15 @@ typedef struct spt_config {
                                        +8 %); 0: such jobs keep the per-cast
                                        wavefront with wavefront_paths in flight.  The image does not
                                        depend on it                                           [0..1] */
-    uint64_t fit_bytes;             /* device memory a fitting job's path queues and hit records may
-                                       take per working set (2 x 16 B x planes + 16 B per path);
-                                       fit_paths shrinks to what fits (more sample chunks; below
-                                       one chunk of the tile's pixels the per-cast wavefront).
-                                       0: the free device memory plus what the caller's set holds,
-                                       less 1/16 (processes or scenes sharing the GPU).  The image
-                                       does not depend on it                                   */
+    uint64_t fit_bytes;             /* device memory a fitting job's path queues, hit records and
+                                       film chunk may take per working set (2 x 16 B x planes +
+                                       16 B + the film slot per path); fit_paths shrinks to what
+                                       fits (more sample chunks; below one chunk of the tile's
+                                       pixels the per-cast wavefront).  0: the free device memory
+                                       plus what the caller's set holds, less 1/16 (processes or
+                                       scenes sharing the GPU); an allocation that fails anyway
+                                       halves the fit and retries.  The image does not depend on
+                                       it                                                      */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

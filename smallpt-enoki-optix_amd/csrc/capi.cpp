@@ -1902,6 +1902,10 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // both.  Config 1, Mpaths/s: 8M 3235, 12M 3470, 16M 3463, 24M 3755,
     // 32M 3715, 48M 3722; configs 2 / 3 / 4: 8M 1712 / 3824 / 851 against
     // 32M 1790 / 4080 / 860.  Default: spt_config.wavefront_paths = 32M.
+    // (a fitting job whose working set could not be allocated comes back here
+    // with half the fit: fit_limit)
+    uint64_t fit_limit = UINT64_MAX;
+retry_fit:
     uint64_t C = p.wavefront_paths ? p.wavefront_paths : cfg.wavefront_paths;
 
     // Pipeline: the wavefront (isect / shade / refill over path queues, the
@@ -1947,19 +1951,22 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     const bool unit = sc->albedo_unit && sc->ntex == 0 && sc->nsph == 0 && sc->nkind == 0;
     const int mode = sc->emission ? kModeEmit : (unit ? kModeUnit : kModeAlbedo);
     const uint64_t film_unit = mode_film_bytes(mode);
-    // A fitting job's queues and hit records must fit in device memory
-    // (spt_config.fit_bytes; 0: the free memory plus what this caller's set
-    // holds, less 1/16 — processes or scenes sharing the GPU): fit_paths
+    // A fitting job's queues, hit records and film chunk must fit in device
+    // memory (spt_config.fit_bytes; 0: the free memory plus what this caller's
+    // set holds, less 1/16 — processes or scenes sharing the GPU): fit_paths
     // shrinks to what fits, into more sample chunks, and below one chunk of
     // the tile's pixels the job keeps the per-cast wavefront.  Asked only when
-    // the set must grow.
-    uint64_t fit_paths = cfg.fit_paths;
+    // the set must grow; an allocation that fails all the same (another
+    // process took the memory in between) halves the fit and tries again.
+    uint64_t fit_paths = std::min<uint64_t>(cfg.fit_paths, fit_limit);
     if (fit_paths && !fused) {
-        const uint64_t per_path = 2ull * 16 * mode_planes(mode) + kHitBytes;
+        const uint64_t per_path = 2ull * 16 * mode_planes(mode) + kHitBytes + film_unit;
         const uint64_t want = std::min<uint64_t>(fit_paths, P * p.spp) * per_path;
         uint64_t held = 0;
-        if (const WorkSet* hs = sc->ws.bound_set(caller))
+        if (const WorkSet* hs = sc->ws.bound_set(caller)) {
             for (const Sub& b : hs->sub) held += (uint64_t)b.cap * (2ull * 16 * b.planes + kHitBytes);
+            held += hs->film_cap;
+        }
         uint64_t room = cfg.fit_bytes;
         if (!room && want > held) {
             size_t fr = 0, tot = 0;
@@ -2032,6 +2039,11 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     ws.last_ticket = sc->ws.next_ticket;
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P,
                           own_queues);
+    if (st == SPT_ERR_OOM && fit && fit_paths > 1) {
+        (void)hipGetLastError();
+        fit_limit = fit_paths / 2;
+        goto retry_fit;
+    }
     if (st) return st;
     // the set's stream 0 (its own): the render's first and last launches, the
     // fork and join of the other sub-wavefronts

@@ -214,16 +214,16 @@ def test_fit_chunks_bitexact(mesh, mode, chunks, monkeypatch):
 
 @pytest.mark.parametrize("mode", ["unit", "emit_spheres"])
 def test_fit_bytes_shrinks_fit(mesh, mode, monkeypatch):
-    """spt_config.fit_bytes: a fitting job whose queues and hit records would
-    exceed it runs with fit_paths cut to what fits (here 2 of 5 samples' paths
+    """spt_config.fit_bytes: a fitting job whose queues, hit records and film
+    would exceed it runs with fit_paths cut to what fits (here 2 of 5 samples' paths
     per chunk), and with less than one chunk of the tile's pixels on the
     per-cast wavefront.  fit_bytes 0 asks the device for its free memory (the
     default, a full fit here).  Same bits every way."""
     for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
         monkeypatch.delenv(k)
     mat = materials(mesh, mode)
-    planes = 2 if mode == "unit" else 4
-    per_path = 2 * 16 * planes + 16  # two queues of `planes` 16-B planes + the hit record
+    planes, film = (2, 1) if mode == "unit" else (4, 12)
+    per_path = 2 * 16 * planes + 16 + film  # two queues of `planes` 16-B planes, the hit record, the film slot
     kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
     spp = 5
     osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
