@@ -58,6 +58,8 @@ double now_ms() {
 // Path queue planes (spt_internal.h PathQueue): 2 (unit), 3 (albedo) or 4
 // (emitters) 16-B quads per path.
 constexpr size_t kHitBytes = 16;
+// an out-of-memory render retries with half its paths in flight down to this many
+constexpr uint64_t kMinRetryPaths = 1u << 16;
 
 // Planes are `stride` elements apart (stride = cap + pad, see queue_stride).
 PathQueue carve_queue(char* base, size_t stride, uint32_t planes) {
@@ -1902,8 +1904,8 @@ spt_status spt_render_async(spt_scene sc, const spt_render_params* pp, float* fi
     // both.  Config 1, Mpaths/s: 8M 3235, 12M 3470, 16M 3463, 24M 3755,
     // 32M 3715, 48M 3722; configs 2 / 3 / 4: 8M 1712 / 3824 / 851 against
     // 32M 1790 / 4080 / 860.  Default: spt_config.wavefront_paths = 32M.
-    // (a fitting job whose working set could not be allocated comes back here
-    // with half the fit: fit_limit)
+    // (a render whose working set could not be allocated comes back here with
+    // half its paths in flight as the limit: fit_limit)
     uint64_t fit_limit = UINT64_MAX;
 retry_fit:
     uint64_t C = p.wavefront_paths ? p.wavefront_paths : cfg.wavefront_paths;
@@ -1959,6 +1961,7 @@ retry_fit:
     // the set must grow; an allocation that fails all the same (another
     // process took the memory in between) halves the fit and tries again.
     uint64_t fit_paths = std::min<uint64_t>(cfg.fit_paths, fit_limit);
+    uint64_t mem_paths = fit_limit;  // paths in flight the memory allows (queues + film chunk)
     if (fit_paths && !fused) {
         const uint64_t per_path = 2ull * 16 * mode_planes(mode) + kHitBytes + film_unit;
         const uint64_t want = std::min<uint64_t>(fit_paths, P * p.spp) * per_path;
@@ -1975,7 +1978,7 @@ retry_fit:
             else
                 (void)hipGetLastError();
         }
-        if (room && want > room) fit_paths = room / per_path;
+        if (room && want > room) mem_paths = fit_paths = std::max<uint64_t>(1, room / per_path);
     }
     rs.fit_paths = fit_paths;
     const bool fit_ok = !fused && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths && fit_paths &&
@@ -2004,7 +2007,7 @@ retry_fit:
     if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
         C = kPixelMajorWavefrontPaths;
     if (fit) C = fit_chunk ? (uint64_t)fit_chunk * P : P * p.spp;
-    C = std::max<uint64_t>(1, std::min<uint64_t>(C, P * p.spp));
+    C = std::max<uint64_t>(1, std::min<uint64_t>(std::min<uint64_t>(C, mem_paths), P * p.spp));
     if (C >= (1ull << 31)) return fail(SPT_ERR_LIMIT, "spt_render: wavefront of %llu paths exceeds 2^31",
                                        (unsigned long long)C);
     // The wavefront is split into K sub-wavefronts on their own streams, so one
@@ -2034,14 +2037,16 @@ retry_fit:
     uint32_t chunk = (uint32_t)std::max<uint64_t>(
         1, std::min<uint64_t>(std::min<uint64_t>(p.spp, budget / (film_unit * P)), 0x7fffffffull / P));
     if (fit_chunk) chunk = std::min(chunk, fit_chunk);  // each chunk fits in flight
+    if (mem_paths != UINT64_MAX) chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(chunk, mem_paths / P));
     rs.paths_in_flight = (uint32_t)C;
     WorkSet& ws = sc->ws.pick_set(caller);
     ws.last_ticket = sc->ws.next_ticket;
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P,
                           own_queues);
-    if (st == SPT_ERR_OOM && fit && fit_paths > 1) {
+    if (st == SPT_ERR_OOM && !fused && C > kMinRetryPaths) {
+        // the fit, or below it the per-cast wavefront and its film chunk, halved
         (void)hipGetLastError();
-        fit_limit = fit_paths / 2;
+        fit_limit = C / 2;
         goto retry_fit;
     }
     if (st) return st;

@@ -241,5 +241,5 @@ def test_fit_bytes_shrinks_fit(mesh, mode, monkeypatch):
         assert st["fit_paths"] == fit_paths, (fit_bytes, st["fit_paths"])
         if in_flight is not None:  # fitting (chunks): every chunk's paths in flight, first cast in lockstep
             assert st["paths_in_flight"] == in_flight and st["lockstep_casts"] > 0
-        else:  # below one chunk of the tile's pixels: the per-cast wavefront, no lockstep cast
-            assert st["lockstep_casts"] == 0
+        else:  # below one chunk of the tile's pixels: the per-cast wavefront, as many paths in flight
+            assert st["lockstep_casts"] == 0 and st["paths_in_flight"] == fit_paths
