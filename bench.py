@@ -231,7 +231,15 @@ def main():
     # lets N ranks share the GPUs there are, to rehearse the N-rank flow on a
     # one-GPU box; the default is strict one-rank-per-device over RCCL.
     if os.environ.get("SPT_REHEARSE_SHARED_GPU") == "1":
-        local = local % max(1, torch.cuda.device_count())
+        ndev = max(1, torch.cuda.device_count())
+        local = local % ndev
+        # the ranks on one device split its memory: each rank's two working
+        # sets get an equal share of 3/4 of it for a fitting job (spt_config.fit_bytes;
+        # the library's own free-memory check races when all ranks start at once)
+        if "SPT_FIT_BYTES" not in os.environ:
+            share = (world + ndev - 1) // ndev
+            total = torch.cuda.get_device_properties(local).total_memory
+            os.environ["SPT_FIT_BYTES"] = str(total * 3 // 4 // (2 * share))
     torch.cuda.set_device(local)
     if world > 1:
         backend = os.environ.get("SPT_DIST_BACKEND", "nccl")
