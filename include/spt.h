@@ -149,6 +149,8 @@ typedef struct spt_render_stats {
                                    (spt_config.lockstep_first), part of the isect launches' casts */
     uint64_t fit_paths;         /* the fit size in effect: spt_config.fit_paths, or fewer when the
                                    queues would not fit in device memory (spt_config.fit_bytes) */
+    uint64_t fit_retries;       /* working-set allocations that failed and were retried with half
+                                   the paths in flight (device memory taken by someone else) */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -294,8 +296,11 @@ typedef struct spt_config {
                                        length, this many casts after the stream's last work
                                        item started, and ends the stream's launches; 0: only
                                        on a short queue                                  [0..64] */
-    uint32_t fit_streams;           /* sub-wavefronts of a job that fits in flight (below), 2; 1 on
-                                       a caller's null stream (shared hardware queues)        [1..4] */
+    uint32_t fit_streams;           /* sub-wavefronts of a job that fits in flight (below), 1: one
+                                       camera cast and one drain over the whole job (two concurrent
+                                       persistent drains split the chip unevenly: the older launch's
+                                       waves win issue); always 1 on a caller's null
+                                       stream (shared hardware queues)                        [1..4] */
     uint64_t fit_paths;             /* a job of at most this many paths (tile px x spp) starts every
                                        path in the first refill (paths in flight = the job, unless
                                        params.wavefront_paths or config.wavefront_paths is set) on fit_streams
@@ -313,12 +318,17 @@ typedef struct spt_config {
                                        octant and the origin's Morton code (coherent bounce rays
                                        per wave; wide-BVH scenes); 0: queue order.  The image does
                                        not depend on it                                       [0..1] */
-    uint32_t lockstep_first;        /* 1: the first cast of a job that fits in flight (fit_paths) runs in
-                                       a one-lane-per-ray isect kernel without lane refill: coherent
-                                       camera rays finish together, so the persistent kernel's refill
-                                       only costs (config 1 +10 %); 0: the persistent
-                                       isect kernel for every cast.  The image does not depend on it
-                                                                                               [0..1] */
+    uint32_t lockstep_first;        /* the first cast of a job that fits in flight (fit_paths): 1: a
+                                       one-lane-per-ray isect kernel without lane refill (coherent
+                                       camera rays finish together), then the shade kernel; 2: one
+                                       camera-cast kernel that makes the camera rays, traces them in
+                                       lockstep and shades the hits (no queue round trip); 3: the
+                                       same with its survivors compacted per XCD shard and the
+                                       drain's per-XCD pools over those segments (one queue counter
+                                       takes ~88 atomics per us; config 1 +11 % over 1, a single
+                                       render +18 %); 0: the persistent isect kernel
+                                       for every cast.  Wide-BVH scenes (2 and 3; BVH2 scenes run
+                                       1).  The image does not depend on it                 [0..3] */
     uint32_t fit_chunks;            /* 1: a job of more than fit_paths paths whose tile has at most
                                        fit_paths pixels runs as sample chunks of at most fit_paths
                                        paths, each started at once like a fitting job (config 3
@@ -517,6 +527,15 @@ const char* spt_version(void);
 /* A hash of the sources and compiler flags this library was built from: profile
  * data (profiles/isect_pmc.json) names the build it measured by this id. */
 const char* spt_build_id(void);
+/* Test hook (not for production use): the working-set allocation numbered
+ * `nth` (0-based, counted over the device allocations spt_render makes for its
+ * path queues, hit records, counters, film chunk and running sum, from this
+ * call on, in any scene) fails with an out-of-memory error once, as when another
+ * process took the memory between the fit rule's check and the allocation;
+ * nth < 0 disarms it.  Lets a test drive the render's halve-and-retry path
+ * (spt_render_stats.fit_retries) deterministically, without exhausting the
+ * device. */
+void spt_debug_fail_workspace_alloc(int32_t nth);
 
 /* ------------------------------------------------------------------ host */
 /* load_meshes (main.cpp:141-251): triangulating OBJ reader with tinyobj's

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cerrno>
@@ -20,6 +21,29 @@
 #include "gpu_build.h"
 #include "host_error.h"
 #include "spt_internal.h"
+
+// Diagnostic build only (make BUILD=build_dbg EXTRA="-g -DSPT_SEGV_TRACE=1"):
+// a host segmentation fault prints the native backtrace (library offsets for
+// addr2line) before the default action.  Not in the product build.
+#ifndef SPT_SEGV_TRACE
+#define SPT_SEGV_TRACE 0
+#endif
+#if SPT_SEGV_TRACE
+#include <execinfo.h>
+#include <signal.h>
+namespace {
+void segv_trace(int sig) {
+    void* bt[64];
+    const int n = backtrace(bt, 64);
+    backtrace_symbols_fd(bt, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct SegvTraceInstall {
+    SegvTraceInstall() { signal(SIGSEGV, segv_trace); }
+} segv_trace_install;
+}  // namespace
+#endif
 
 using namespace spt;
 
@@ -90,6 +114,7 @@ struct Counters {
     uint32_t pad[2];
     alignas(128) uint32_t isect_next_b;  // SPT_ISECT_CAMERA: the counter of the launches on queue 1
     alignas(128) uint32_t xcd_next[8][32];  // the drain / fused kernel's per-XCD work counters (one line each)
+    alignas(128) uint32_t surv_shard[kShards][kShardStride];  // a sharded camera cast's survivors per shard
 };
 uint32_t* isect_next_of(Counters* c, int queue) { return queue ? &c->isect_next_b : &c->isect_next; }
 
@@ -458,6 +483,19 @@ hipError_t create_sub_stream(hipStream_t* s, bool own_queue) {
     return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
 }
 
+// spt_debug_fail_workspace_alloc: the allocation that fails once (-1: none)
+std::atomic<int32_t> g_fail_ws_alloc{-1};
+hipError_t ws_malloc(void** p, size_t bytes) {
+    int32_t n = g_fail_ws_alloc.load();
+    while (n >= 0 && !g_fail_ws_alloc.compare_exchange_weak(n, n - 1)) {
+    }
+    if (n == 0) {
+        *p = nullptr;
+        return hipErrorOutOfMemory;
+    }
+    return hipMalloc(p, bytes);
+}
+
 spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uint32_t planes, size_t film_bytes,
                             size_t acc_floats, bool own_queues) {
     bool quiet = !ws.used;
@@ -473,14 +511,14 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
             if ((st = quiesce())) return st;
             hfree(b.qa); hfree(b.qb); hfree(b.hits);
             b.cap = 0;
-            HIP_TRY(hipMalloc((void**)&b.qa, (size_t)16 * planes * queue_stride(cap, pad)));
-            HIP_TRY(hipMalloc((void**)&b.qb, (size_t)16 * planes * queue_stride(cap, pad)));
-            HIP_TRY(hipMalloc((void**)&b.hits, kHitBytes * cap));
+            HIP_TRY(ws_malloc((void**)&b.qa, (size_t)16 * planes * queue_stride(cap, pad)));
+            HIP_TRY(ws_malloc((void**)&b.qb, (size_t)16 * planes * queue_stride(cap, pad)));
+            HIP_TRY(ws_malloc((void**)&b.hits, kHitBytes * cap));
             b.cap = cap;
             b.pad = pad;
             b.planes = planes;
         }
-        if (!b.cnt) HIP_TRY(hipMalloc((void**)&b.cnt, sizeof(Counters)));
+        if (!b.cnt) HIP_TRY(ws_malloc((void**)&b.cnt, sizeof(Counters)));
         if (!b.host_cnt) HIP_TRY(hipHostMalloc((void**)&b.host_cnt, 2 * sizeof(Counters), hipHostMallocDefault));
         for (auto& e : b.count_ev)
             if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -499,19 +537,35 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
         if ((st = quiesce())) return st;
         hfree(ws.film);
         ws.film_cap = 0;
-        HIP_TRY(hipMalloc((void**)&ws.film, film_bytes));
+        HIP_TRY(ws_malloc((void**)&ws.film, film_bytes));
         ws.film_cap = film_bytes;
     }
     if (acc_floats > ws.acc_cap) {
         if ((st = quiesce())) return st;
         hfree(ws.acc);
         ws.acc_cap = 0;
-        HIP_TRY(hipMalloc((void**)&ws.acc, sizeof(float) * acc_floats));
+        HIP_TRY(ws_malloc((void**)&ws.acc, sizeof(float) * acc_floats));
         ws.acc_cap = acc_floats;
     }
     if (!ws.fork_ev) HIP_TRY(hipEventCreateWithFlags(&ws.fork_ev, hipEventDisableTiming));
     if (!ws.free_ev) HIP_TRY(hipEventCreateWithFlags(&ws.free_ev, hipEventDisableTiming));
     if (!ws.call_ev) HIP_TRY(hipEventCreateWithFlags(&ws.call_ev, hipEventDisableTiming));
+    return SPT_OK;
+}
+
+// After an allocation that failed: the set's path queues, hit records and film
+// chunk are freed (once its last render has finished with them), so a retry
+// with fewer paths in flight allocates from scratch.  Streams, counters and
+// events stay.
+spt_status release_queues(WorkSet& ws) {
+    if (ws.used) HIP_TRY(hipEventSynchronize(ws.free_ev));
+    for (Sub& b : ws.sub) {
+        hfree(b.qa); hfree(b.qb); hfree(b.hits);
+        b.cap = 0;
+        b.planes = 0;
+    }
+    hfree(ws.film);
+    ws.film_cap = 0;
     return SPT_OK;
 }
 
@@ -735,7 +789,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(fit_paths, 0, 1ull << 31)
     CFG_RANGE(sub_queues, 0, 1)
     CFG_RANGE(drain_sort, 0, 1)
-    CFG_RANGE(lockstep_first, 0, 1)
+    CFG_RANGE(lockstep_first, 0, 3)
     CFG_RANGE(fit_chunks, 0, 1)
 #undef CFG_RANGE
     return SPT_OK;
@@ -851,6 +905,8 @@ const char* spt_version(void) { return "spt-mi355x 0.1 (gfx950 wavefront path tr
 #define SPT_BUILD_ID "unknown"
 #endif
 const char* spt_build_id(void) { return SPT_BUILD_ID; }
+
+void spt_debug_fail_workspace_alloc(int32_t nth) { g_fail_ws_alloc.store(nth < 0 ? -1 : nth); }
 
 spt_status spt_init(int32_t device) {
     spt_status st = ensure_device();
@@ -1133,11 +1189,11 @@ void spt_default_config(spt_config* c) {
     c->drain_q8 = kDefaultDrainQ8;
     c->drain_grid_q8 = 0;
     c->drain_casts = kDefaultDrainCasts;
-    c->fit_streams = 2;
+    c->fit_streams = 1;
     c->fit_paths = kDefaultFitPaths;
     c->sub_queues = 1;
     c->drain_sort = 0;
-    c->lockstep_first = 1;
+    c->lockstep_first = 3;
     c->fit_chunks = 1;
 }
 
@@ -1960,14 +2016,26 @@ retry_fit:
     // the tile's pixels the job keeps the per-cast wavefront.  Asked only when
     // the set must grow; an allocation that fails all the same (another
     // process took the memory in between) halves the fit and tries again.
+    // (the set's streams, below: a caller's null stream gets plain streams and
+    // a fitting job one sub-wavefront on them)
+    const bool null_caller = caller == nullptr || caller == hipStreamLegacy || caller == hipStreamPerThread;
+    const bool own_queues = cfg.sub_queues != 0 && !null_caller;
     uint64_t fit_paths = std::min<uint64_t>(cfg.fit_paths, fit_limit);
     uint64_t mem_paths = fit_limit;  // paths in flight the memory allows (queues + film chunk)
     if (fit_paths && !fused) {
         const uint64_t per_path = 2ull * 16 * mode_planes(mode) + kHitBytes + film_unit;
         const uint64_t want = std::min<uint64_t>(fit_paths, P * p.spp) * per_path;
+        // what this render may reuse of the set it will get: the queues and hit
+        // records of the sub-wavefronts a fitting job runs on (as allocated,
+        // plane padding included) and the film chunk; a sub-wavefront beyond
+        // those keeps its buffers and is not counted
         uint64_t held = 0;
         if (const WorkSet* hs = sc->ws.bound_set(caller)) {
-            for (const Sub& b : hs->sub) held += (uint64_t)b.cap * (2ull * 16 * b.planes + kHitBytes);
+            const int kf = own_queues ? (int)cfg.fit_streams : 1;
+            for (int k = 0; k < kf && k < kMaxStreams; k++) {
+                const Sub& b = hs->sub[k];
+                held += 2ull * 16 * b.planes * queue_stride(b.cap, b.pad) + (uint64_t)kHitBytes * b.cap;
+            }
             held += hs->film_cap;
         }
         uint64_t room = cfg.fit_bytes;
@@ -2023,8 +2091,6 @@ retry_fit:
     // streams, which share the process's GPU_MAX_HW_QUEUES, and a fitting job
     // then runs on one sub-wavefront: more would share queues with the other
     // set's and serialise behind them.
-    const bool null_caller = caller == nullptr || caller == hipStreamLegacy || caller == hipStreamPerThread;
-    const bool own_queues = cfg.sub_queues != 0 && !null_caller;
     int K = fused ? 1 : fit ? (own_queues ? (int)cfg.fit_streams : 1) : (int)cfg.streams;
     if (fused) C = 64;  // no queues
     if ((uint64_t)K > C) K = (int)C;
@@ -2044,8 +2110,13 @@ retry_fit:
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P,
                           own_queues);
     if (st == SPT_ERR_OOM && !fused && C > kMinRetryPaths) {
-        // the fit, or below it the per-cast wavefront and its film chunk, halved
+        // the fit, or below it the per-cast wavefront and its film chunk, halved;
+        // first the queues, hit records and film chunk this attempt allocated
+        // (ensure_workspace only grows them) are freed, so the halved attempt
+        // holds half, not more
         (void)hipGetLastError();
+        if ((st = release_queues(ws))) return st;
+        rs.fit_retries++;
         fit_limit = C / 2;
         goto retry_fit;
     }
@@ -2156,6 +2227,12 @@ retry_fit:
     const bool lane_xcd = (cfg.xcd_remap & 4u) != 0;
     // spt_config.drain_sort: a forced drain takes its queue sorted (wide-BVH scenes)
     const bool drain_sort = drain_on && cfg.drain_sort != 0 && sc->nodes8 != nullptr;
+    // spt_config.lockstep_first = 2: the lockstep first cast also makes its
+    // camera rays and shades its hits in the same launch (camera_cast_kernel;
+    // wide-BVH scenes): no queue round trip for the first cast
+    const bool cam_cast = cfg.lockstep_first >= 2 && sc->nodes8 != nullptr;
+    // = 3: its survivors compacted per XCD shard, the drain's pools per shard
+    const bool cam_shards = cam_cast && cfg.lockstep_first >= 3;
     uint64_t drain_launches = 0;
     PathQueue q[kMaxStreams][2];
     for (int k = 0; k < K; k++) {
@@ -2206,6 +2283,8 @@ retry_fit:
         R.isect_next = &b.cnt->isect_next;
         R.exhausted = &b.cnt->exhausted;
         R.xcd_next = lane_xcd ? &b.cnt->xcd_next[0][0] : nullptr;
+        R.book_only = 0;
+        R.surv_shards = nullptr;
         I.drain_below = 0;
         S.drain_below = 0;
         if (drain_on) {
@@ -2235,7 +2314,9 @@ retry_fit:
             D.grid_q8 = cfg.drain_grid_q8 ? cfg.drain_grid_q8 : 256u / (uint32_t)K;
             D.env_r = p.env[0]; D.env_g = p.env[1]; D.env_b = p.env[2];
             D.nt = queue_nt;
+            D.seg_count = nullptr;
         }
+        S.shard_items = 0;
     }
 
     uint64_t iters = 0;
@@ -2310,6 +2391,8 @@ retry_fit:
             ra[k].work_end = we;
             sa[k].sample0 = s0; sa[k].chunk_ns = ns;
             da[k].sample0 = s0; da[k].pm_ns = pixel_major ? ns : 0;  // the shade's film layout
+            da[k].seg_count = nullptr;  // (set by a sharded camera cast of this chunk)
+            da[k].xcd_next = lane_xcd ? &b.cnt->xcd_next[0][0] : nullptr;
             // the first refill starts at the sub-wavefront's first work item
             ra[k].q = q[k][0]; ra[k].surv = &b.cnt->surv[0]; ra[k].cursor_in = nullptr; ra[k].cursor_init = wb;
             ra[k].cursor_out = &b.cnt->cursor[0]; ra[k].qn_out = &b.cnt->qn[0];
@@ -2321,9 +2404,13 @@ retry_fit:
             sub_end[k] = we;
             started[k] = wb + first;
             lock0[k] = cfg.lockstep_first && fit && drain_on && !trav_stats && first >= drain_T[k];
-            // (SPT_ISECT_CAMERA: the first isect launch starts these paths)
-            if (!kIsectCam && (st = mark(0, strm[k], [&] { return launch_refill(ra[k], first, strm[k]); })))
+            // (SPT_ISECT_CAMERA: the first isect launch starts these paths; the
+            // camera cast makes them itself: the refill only keeps the books)
+            ra[k].book_only = lock0[k] && cam_cast ? 1u : 0u;
+            if (!kIsectCam &&
+                (st = mark(0, strm[k], [&] { return launch_refill(ra[k], ra[k].book_only ? 1u : first, strm[k]); })))
                 return st;
+            ra[k].book_only = 0;
         }
         // isect -> shade -> refill per sub-wavefront until every queue drains.
         // A path cast in iteration i was started by the refill after iteration
@@ -2441,7 +2528,33 @@ retry_fit:
                     }
                     const bool lockstep = it == 0 && lock0[k];
                     if (lockstep) rs.lockstep_casts += known[k];
-                    if ((st = mark(1, strm[k], [&] {
+                    // sharded survivors (spt_internal.h kShards): when the camera cast
+                    // holds the sub-wavefront's every path and the drain takes the
+                    // queue next, its per-XCD pools over the same segments
+                    bool sharded = false;
+                    if (lockstep && cam_cast) {
+                        // the first cast, camera ray to shade, in one launch; survivors
+                        // into queue nx (surv[nx] zeroed with the counters), the
+                        // refill below keeps the books as after a shade
+                        sharded = cam_shards && started[k] >= sub_end[k] && cfg.drain_casts == 1 && !drain_sort;
+                        CameraCastArgs ca;
+                        ca.r = ra[k];  // the first refill's work items (cursor_init: the share's start)
+                        ca.s = sa[k];
+                        ca.s.in = q[k][c];
+                        ca.s.out = q[k][nx];
+                        ca.s.hits = nullptr;
+                        ca.s.count_in = &b.cnt->qn[c];
+                        ca.s.count_out = sharded ? &b.cnt->surv_shard[0][0] : &b.cnt->surv[nx];
+                        ca.s.shard_items = sharded ? known[k] : 0u;
+                        ca.n = known[k];
+                        if ((st = mark(1, strm[k], [&] { return launch_camera_cast(ca, mode, strm[k]); }))) return st;
+                        if (sharded) {
+                            da[k].seg_count = &b.cnt->surv_shard[0][0];
+                            da[k].seg_items = known[k];
+                            da[k].seg_block = kIsectBlock;
+                            da[k].xcd_next = &b.cnt->xcd_next[0][0];
+                        }
+                    } else if ((st = mark(1, strm[k], [&] {
                              if (lockstep) return launch_isect_lockstep(ia[k], known[k], strm[k]);
                              return trav_stats ? launch_isect_queue_stats(ia[k], known[k], strm[k])
                                                : cam ? launch_isect_queue_cam(ia[k], known[k], strm[k])
@@ -2452,7 +2565,9 @@ retry_fit:
                     sa[k].in = q[k][c]; sa[k].out = q[k][nx];
                     sa[k].count_in = &b.cnt->qn[c];
                     sa[k].count_out = &b.cnt->surv[nx];
-                    if ((st = mark(2, strm[k], [&] { return launch_shade(sa[k], mode, known[k], strm[k]); }))) return st;
+                    if (!(lockstep && cam_cast) &&
+                        (st = mark(2, strm[k], [&] { return launch_shade(sa[k], mode, known[k], strm[k]); })))
+                        return st;
                     // (at a chunk's first iteration the count is known exactly: no
                     // conditional drain when it cannot be short)
                     if (dph && !(it == 0 && known[k] >= drain_T[k])) {
@@ -2472,11 +2587,20 @@ retry_fit:
                     ra[k].surv_clear = &b.cnt->surv[c];
                     ra[k].casts_in = &b.cnt->qn[c];
                     ra[k].iter_tag = (uint32_t)it + 2;
+                    // (after a sharded camera cast: its survivors are the shards' sum, and
+                    // the drain's per-XCD pool counters start at zero)
+                    uint32_t* const xcd_keep = ra[k].xcd_next;
+                    if (sharded) {
+                        ra[k].surv_shards = &b.cnt->surv_shard[0][0];
+                        ra[k].xcd_next = &b.cnt->xcd_next[0][0];
+                    }
                     // new paths: at most the work not yet known to be started (one
                     // block still runs to carry the counters over)
                     const uint32_t fill = (uint32_t)std::min<uint64_t>(b.cap, sub_end[k] - started[k]);
                     if ((st = mark(0, strm[k], [&] { return launch_refill(ra[k], fill, strm[k]); })))
                         return st;
+                    ra[k].surv_shards = nullptr;
+                    ra[k].xcd_next = xcd_keep;
                     cur[k] = nx;
                 }
                 it++;

@@ -105,6 +105,25 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #define SPT_DRAIN_WAVES_NT 6
 #endif
 
+// Diagnostic build only (make BUILD=build_wlog EXTRA=-DSPT_WAVE_LOG=1,
+// tools/wave_log.py): every wave of a lane-loop launch (fused kernel, drain)
+// records its start and end on the 100-MHz wall clock, the HW_ID / XCC_ID
+// registers (CU, SIMD, SE, hardware queue, XCD), the launch's queue-count
+// address (which sub-wavefront) and the paths it shaded.  Read back with
+// spt_debug_wave_log (below).  Not in the product build.
+#ifndef SPT_WAVE_LOG
+#define SPT_WAVE_LOG 0
+#endif
+#if SPT_WAVE_LOG
+struct WaveRec {
+    unsigned long long t0, t1;
+    uint32_t hw, xcc, tag, casts, block, drain;
+};
+constexpr uint32_t kWaveLogMax = 1u << 18;
+__device__ uint32_t g_wlog_n;
+__device__ WaveRec g_wlog[kWaveLogMax];
+#endif
+
 // ------------------------------------------------------------- traversal
 // Triangle records (spt_internal.h): vertex i of slot s rotated by r starts at
 // float 5 i + r, the original id is float 15.
@@ -1085,7 +1104,11 @@ __device__ __forceinline__ Pcg32 path_rng(uint32_t gpix, const PcgJump& js, cons
 constexpr uint32_t kRefillMaxBlocks = SPT_REFILL_MAX_BLOCKS;
 template <int kMode, bool kNt = false>
 __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
-    const uint32_t surv = *a.surv;
+    uint32_t surv = 0;
+    if (a.surv_shards)
+        for (uint32_t j = 0; j < kShards; j++) surv += a.surv_shards[j * kShardStride];
+    else
+        surv = *a.surv;
     const uint64_t cur = a.cursor_in ? *a.cursor_in : a.cursor_init;
     const uint64_t avail = a.work_end > cur ? a.work_end - cur : 0;
     const uint32_t room = a.capacity - surv;
@@ -1106,6 +1129,7 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
         }
         if (total) atomicAdd(&a.stats[2], (unsigned long long)total);
     }
+    if (a.book_only) return;
 #if SPT_REFILL_STRIDE
     for (uint32_t j = i; j < total; j += gridDim.x * 256u) {
 #else
@@ -1141,17 +1165,28 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 // that work.
 // kSpt: the scene has smallpt spheres or mirror / glass materials (a separate
 // instance, so plain scenes keep the leaner register budget).
-template <int kMode, bool kSpt, bool kNt = false>
-__global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
-    __shared__ uint32_t s_wave_cnt[kShadeBlock / 64];
-    __shared__ uint32_t s_wave_off[kShadeBlock / 64];
+//
+// shade_block is the whole of it for one block of kBlock threads, each holding
+// one path or none (valid): the path's queue entry, hit record and (albedo /
+// emitter modes) throughput and radiance come from Src — the queue and the
+// hit records in shade_kernel, registers in camera_cast_kernel (the first
+// cast, traced in the same launch) — so both run the same arithmetic and
+// compaction.  Every thread of the block must call it (barriers, ballots).
+template <bool kNt>
+struct QueueSrc {  // shade_kernel: queue slot i of a.in and its hit record
+    const ShadeArgs& a;
+    uint32_t i;
+    __device__ __forceinline__ float4 q1() const { return ldq<kNt>(a.in.q1 + i); }
+    __device__ __forceinline__ float4 q2() const { return ldq<kNt>(a.in.q2 + i); }
+    __device__ __forceinline__ float4 hit() const { return ldq<kNt>(a.hits + i); }
+    __device__ __forceinline__ float4 q0() const { return ldq<kNt>(a.in.q0 + i); }
+    __device__ __forceinline__ float2 rad() const { return ldq2<kNt>(a.in.rad + i); }
+};
+template <int kMode, bool kSpt, bool kNt, uint32_t kBlock, typename Src>
+__device__ __forceinline__ void shade_block(const ShadeArgs& a, bool valid, const Src& src) {
+    __shared__ uint32_t s_wave_cnt[kBlock / 64];
+    __shared__ uint32_t s_wave_off[kBlock / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-    const uint32_t n = *a.count_in;
-    if (n < a.drain_below) return;  // the drain launch takes this queue (launch_drain)
-    // the grid may be sized from a stale (larger) count: remap only the
-    // blocks that hold queued paths, so every XCD gets its eighth of them
-    const uint32_t nreal = min(gridDim.x, (n + kShadeBlock - 1) / kShadeBlock);
-    const uint32_t i = (a.xcd_remap && blockIdx.x < nreal ? xcd_block(blockIdx.x, nreal) : blockIdx.x) * kShadeBlock + tid;
 
     // ---- phase 1: survive or terminate (the bounce inputs load alongside)
     bool emit = false;
@@ -1171,13 +1206,13 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
         o = d = v3(0, 0, 0);
     }
     float tr = 1.0f, tg = 1.0f, tb = 1.0f, lr = 0.0f, lg = 0.0f, lb = 0.0f;
-    if (i < n) {
-        const float4 q1 = ldq<kNt>(a.in.q1 + i), q2 = ldq<kNt>(a.in.q2 + i);
+    if (valid) {
+        const float4 q1 = src.q1(), q2 = src.q2();
         meta = f2u(q1.w);
         pix = f2u(q2.w);
         const uint32_t depth = meta & ((1u << kMetaDepthBits) - 1u);
         const uint32_t sample = meta >> kMetaDepthBits;
-        hit = ldq<kNt>(a.hits + i);
+        hit = src.hit();
         slot = (int32_t)f2u(hit.x);
         if (kSpt && a.sc.nsph) {
             // smallpt's analytic spheres after the triangle BVH (the isect kernel
@@ -1190,11 +1225,11 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
             hit = make_float4(u2f((uint32_t)slot), h.t, h.u, h.v);
         }
         if (kMode >= kModeAlbedo) {
-            const float4 q0 = ldq<kNt>(a.in.q0 + i);
+            const float4 q0 = src.q0();
             tr = q0.x; tg = q0.y; tb = q0.z;
             if (kMode == kModeEmit) lr = q0.w;
         }
-        if (kMode == kModeEmit) { const float2 l = ldq2<kNt>(a.in.rad + i); lg = l.x; lb = l.y; }
+        if (kMode == kModeEmit) { const float2 l = src.rad(); lg = l.x; lb = l.y; }
         bool term = true, escaped = false;
         if (slot == -1) {
             // miss: film += select(!hit && active, contrib, 0)  (main.cpp:407)
@@ -1275,14 +1310,20 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     __syncthreads();
     uint32_t base = 0, total = 0;
     if (tid == 0) {
-        for (uint32_t w = 0; w < kShadeBlock / 64; w++) total += s_wave_cnt[w];
+        for (uint32_t w = 0; w < kBlock / 64; w++) total += s_wave_cnt[w];
         // returns during phase 2.  The address goes through an opaque VGPR
         // zero: for a uniform address the compiler's atomic optimizer wraps
         // the add in a wave scan whose readfirstlane waits for the return
         // right here, serialising the atomic's latency with phase 2.
         uint32_t zero;
         asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
-        if (total) base = atomicAdd(a.count_out + zero, total);
+        if (a.shard_items) {  // the block's shard: its XCD's counter and segment (shard_base)
+            const uint32_t j = blockIdx.x % kShards;
+            if (total) base = atomicAdd(a.count_out + j * kShardStride + zero, total);
+            base += shard_base(j, a.shard_items, kBlock);
+        } else if (total) {
+            base = atomicAdd(a.count_out + zero, total);
+        }
     }
 
     // ---- phase 2: the bounce ray of every survivor
@@ -1311,13 +1352,89 @@ __global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
     }
     if (tid == 0) {
         uint32_t off = base;
-        for (uint32_t w = 0; w < kShadeBlock / 64; w++) {
+        for (uint32_t w = 0; w < kBlock / 64; w++) {
             s_wave_off[w] = off;
             off += s_wave_cnt[w];
         }
     }
     __syncthreads();
     if (emit) store_path<kMode, kNt>(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, tr, tg, tb, lr, lg, lb);
+}
+
+template <int kMode, bool kSpt, bool kNt = false>
+__global__ __launch_bounds__(kShadeBlock) void shade_kernel(ShadeArgs a) {
+    const uint32_t n = *a.count_in;
+    if (n < a.drain_below) return;  // the drain launch takes this queue (launch_drain)
+    // the grid may be sized from a stale (larger) count: remap only the
+    // blocks that hold queued paths, so every XCD gets its eighth of them
+    const uint32_t nreal = min(gridDim.x, (n + kShadeBlock - 1) / kShadeBlock);
+    const uint32_t i =
+        (a.xcd_remap && blockIdx.x < nreal ? xcd_block(blockIdx.x, nreal) : blockIdx.x) * kShadeBlock + threadIdx.x;
+    shade_block<kMode, kSpt, kNt, kShadeBlock>(a, i < n, QueueSrc<kNt>{a, i});
+}
+
+// ----------------------------------------------------------- camera cast
+#ifndef SPT_CAM_RECOMPUTE
+#define SPT_CAM_RECOMPUTE 0
+#endif
+#ifndef SPT_CAM_WAVES
+#define SPT_CAM_WAVES 0  // 0: the tracer's (8 for the 64-B node)
+#endif
+// A fitting job's first cast in one launch (spt_config.camera_cast): one lane
+// per work item of the sub-wavefront — its camera ray (refill_kernel's
+// arithmetic, start_path), its trace in lockstep with the wave's other lanes
+// (isect_lockstep_kernel: a wave holds one pixel's 64 samples in pixel-major
+// order, coherent rays), then its shade (shade_block: film write, or the
+// bounce ray compacted into the drain's queue).  The camera rays and their
+// hit records never touch memory: the refill's 32-B queue write, the isect's
+// 32-B read and 16-B hit write and the shade's 48-B read per path are gone,
+// and so are two launches per render.  Same arithmetic, same bits.
+struct CamSrc {  // the path in registers: its first cast, just traced
+    V3 o, d;
+    uint32_t pix, meta;
+    TraceHit h;
+    __device__ __forceinline__ float4 q1() const { return make_float4(o.x, o.y, o.z, u2f(meta)); }
+    __device__ __forceinline__ float4 q2() const { return make_float4(d.x, d.y, d.z, u2f(pix)); }
+    __device__ __forceinline__ float4 hit() const { return make_float4(u2f((uint32_t)h.slot), h.t, h.u, h.v); }
+    __device__ __forceinline__ float4 q0() const { return make_float4(1.0f, 1.0f, 1.0f, 0.0f); }  // main.cpp:391
+    __device__ __forceinline__ float2 rad() const { return make_float2(0.0f, 0.0f); }
+};
+template <typename Tr, int kMode, bool kSpt, bool kNt>
+__global__ __launch_bounds__(kIsectBlock)
+__attribute__((amdgpu_waves_per_eu(SPT_CAM_WAVES ? SPT_CAM_WAVES : Tr::kMinWaves, 8)))
+void camera_cast_kernel(CameraCastArgs a) {
+    extern __shared__ uint32_t lds_stack[];
+    const Lds L = block_lds(lds_stack);
+    const uint32_t i = blockIdx.x * kIsectBlock + threadIdx.x;
+    const bool valid = i < a.n;
+    CamSrc c;
+    c.o = c.d = v3(0.0f, 0.0f, 0.0f);
+    c.pix = c.meta = 0;
+    c.h.slot = -1;
+    c.h.id = 0xffffffffu;
+    c.h.t = kRayTmax;
+    c.h.u = c.h.v = 0.0f;
+    if (valid) {
+        start_path(a.r, a.r.cursor_init + i, c.o, c.d, c.pix, c.meta);
+        NoStats st;
+        Tr tr;
+        // any-hit for the last cast unless emitters need the surface (isect_queue_kernel)
+        tr.init(a.s.sc, c.o, c.d, kRayTmin, kRayTmax, a.s.max_depth <= 1 && !a.s.sc.emission, L);
+        if (!tr.finished())
+            while (!tr.step(a.s.sc, L, st)) {
+            }
+        c.h = tr.hit(a.s.sc, L);
+#if SPT_CAM_RECOMPUTE
+        // the ray again (the same arithmetic, the same bits) rather than keeping
+        // its direction, pixel and sample live across the traversal: the
+        // traversal keeps its 64 VGPRs (8 waves) with no spill.  The opaque
+        // copy of the work item stops the compiler from reusing the first one.
+        uint32_t w = i;
+        asm volatile("" : "+v"(w));
+        start_path(a.r, a.r.cursor_init + w, c.o, c.d, c.pix, c.meta);
+#endif
+    }
+    shade_block<kMode, kSpt, kNt, kIsectBlock>(a.s, valid, c);
 }
 
 // ------------------------------------------------------------ fused render
@@ -1344,11 +1461,20 @@ __attribute__((amdgpu_waves_per_eu(kDrain && kMode == kModeUnit ? (kNt ? SPT_DRA
                                    : kDrain ? SPT_DRAIN_WAVES_RGB : SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
+#if SPT_WAVE_LOG
+    const unsigned long long wl_t0 = (unsigned long long)wall_clock64();
+#endif
     extern __shared__ uint32_t lds_stack[];
     const Lds L = block_lds(lds_stack);
     uint32_t n = a.count;
     if constexpr (kDrain) {
-        n = wave_uniform(*a.qcount);
+        if (a.seg_count) {  // a sharded queue: the sum of its segments
+            n = 0;
+            for (uint32_t j = 0; j < kShards; j++) n += a.seg_count[j * kShardStride];
+            n = wave_uniform(n);
+        } else {
+            n = wave_uniform(*a.qcount);
+        }
         if (n >= a.drain_below) return;  // the isect and shade launches take this queue
         if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(a.drained, (unsigned long long)n);
     }
@@ -1381,7 +1507,9 @@ void render_fused_kernel(FusedArgs a) {
     const uint32_t nwaves = gridDim.x * (kIsectBlock / 64);
     const uint32_t blk = a.xcd_next ? xcd_block(blockIdx.x, gridDim.x) : blockIdx.x;
     const uint32_t wave_id = wave_uniform(blk * (kIsectBlock / 64) + (threadIdx.x >> 6));
-    const uint32_t share = (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
+    // (a sharded queue's segments are taken only through the per-XCD pools)
+    const uint32_t share =
+        kDrain && a.seg_count ? 0u : (uint32_t)(((uint64_t)n * a.static_share_q8 / 256) / nwaves);
     const uint32_t dyn_base = share * nwaves;
     uint32_t pool = wave_id * share, pool_end = pool + share;
     bool drained = false;
@@ -1492,8 +1620,14 @@ void render_fused_kernel(FusedArgs a) {
                 if (pool == pool_end && a.xcd_next) {
                     // this XCD's eighth of [dyn_base, n), then the next XCD's
                     while (xcd_tries < 8u) {
-                        const uint32_t lo = dyn_base + (uint32_t)((uint64_t)(n - dyn_base) * xcd / 8u);
-                        const uint32_t hi = dyn_base + (uint32_t)((uint64_t)(n - dyn_base) * (xcd + 1u) / 8u);
+                        uint32_t lo, hi;
+                        if (kDrain && a.seg_count) {  // this XCD's segment of a sharded queue
+                            lo = shard_base(xcd, a.seg_items, a.seg_block);
+                            hi = lo + wave_uniform(a.seg_count[xcd * kShardStride]);
+                        } else {
+                            lo = dyn_base + (uint32_t)((uint64_t)(n - dyn_base) * xcd / 8u);
+                            hi = dyn_base + (uint32_t)((uint64_t)(n - dyn_base) * (xcd + 1u) / 8u);
+                        }
                         uint32_t got = 0;
                         if ((threadIdx.x & 63u) == 0) got = atomicAdd(a.xcd_next + xcd * 32u, a.chunk);
                         got = wave_uniform((uint32_t)__shfl((int)got, 0));
@@ -1580,6 +1714,23 @@ void render_fused_kernel(FusedArgs a) {
             pending = true;
         }
     }
+#if SPT_WAVE_LOG
+    if ((threadIdx.x & 63u) == 0) {
+        const uint32_t i = atomicAdd(&g_wlog_n, 1u);
+        if (i < kWaveLogMax) {
+            WaveRec r;
+            r.t0 = wl_t0;
+            r.t1 = (unsigned long long)wall_clock64();
+            r.hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            r.xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+            r.tag = kDrain ? (uint32_t)(uintptr_t)a.qcount : 0u;
+            r.casts = casts;
+            r.block = blockIdx.x;
+            r.drain = kDrain ? 1u : 0u;
+            g_wlog[i] = r;
+        }
+    }
+#endif
     // the drain: a queued path's first cast here was counted with the queue
     // (by the refill that follows), so only the casts after it are added;
     // every cast it traced goes to drained_casts
@@ -1832,6 +1983,35 @@ hipError_t launch_isect_lockstep(const IsectQueueArgs& a, uint32_t grid_items, h
                       : launch_isect_lockstep_t<Tracer8, false>(a, grid_items, s);
 }
 
+template <typename Tr, int kMode, bool kSpt, bool kNt>
+static hipError_t launch_camera_cast_t(const CameraCastArgs& a, hipStream_t s) {
+    const size_t lds = (size_t)a.s.sc.stack_depth * Tr::kStackWords * kIsectBlock * sizeof(uint32_t) + Tr::kExtraLds;
+    hipLaunchKernelGGL((camera_cast_kernel<Tr, kMode, kSpt, kNt>), dim3(blocks_for(a.n, kIsectBlock)),
+                       dim3(kIsectBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+template <typename Tr, bool kNt>
+static hipError_t launch_camera_cast_m(const CameraCastArgs& a, int mode, hipStream_t s) {
+    const bool spt = a.s.sc.nsph || a.s.sc.nkind;  // never in unit mode (launch_shade)
+    if (mode == kModeEmit && spt) return launch_camera_cast_t<Tr, kModeEmit, true, kNt>(a, s);
+    if (mode == kModeEmit) return launch_camera_cast_t<Tr, kModeEmit, false, kNt>(a, s);
+    if (mode == kModeAlbedo && spt) return launch_camera_cast_t<Tr, kModeAlbedo, true, kNt>(a, s);
+    if (mode == kModeAlbedo) return launch_camera_cast_t<Tr, kModeAlbedo, false, kNt>(a, s);
+    return launch_camera_cast_t<Tr, kModeUnit, false, kNt>(a, s);
+}
+
+// wide-BVH scenes only (camera_cast_supported); a.n: the work items, known exactly
+hipError_t launch_camera_cast(const CameraCastArgs& a, int mode, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    if (!a.s.sc.nodes8) return hipErrorInvalidValue;
+    if (a.s.nt)
+        return a.s.sc.node6 ? launch_camera_cast_m<Tracer6, true>(a, mode, s)
+                            : launch_camera_cast_m<Tracer8, true>(a, mode, s);
+    return a.s.sc.node6 ? launch_camera_cast_m<Tracer6, false>(a, mode, s)
+                        : launch_camera_cast_m<Tracer8, false>(a, mode, s);
+}
+
 hipError_t launch_isect_queue_stats(const IsectQueueArgs& a, uint32_t grid_items, hipStream_t s) {
     if (!a.sc.nodes8) return launch_isect_queue_t<Tracer, true>(a, grid_items, s);
     return a.sc.node6 ? launch_isect_queue_t<Tracer6, true>(a, grid_items, s)
@@ -2061,3 +2241,23 @@ hipError_t launch_hit_info(const HitInfoArgs& a, hipStream_t s) {
 }
 
 }  // namespace spt
+
+#if SPT_WAVE_LOG
+// Diagnostic build only: copy up to `max` wave records (8 x 8-byte words each:
+// t0, t1, hw | xcc << 32, tag | casts << 32, block | drain << 32) to `out`,
+// return how many waves logged since the last reset (device synchronised first).
+extern "C" long long spt_debug_wave_log(void* out, unsigned long long max, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    uint32_t n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(spt::g_wlog_n), sizeof(n)) != hipSuccess) return -1;
+    const unsigned long long take = std::min<unsigned long long>(std::min<unsigned long long>(n, spt::kWaveLogMax), max);
+    if (out && take &&
+        hipMemcpyFromSymbol(out, HIP_SYMBOL(spt::g_wlog), take * sizeof(spt::WaveRec)) != hipSuccess)
+        return -1;
+    if (reset) {
+        const uint32_t z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(spt::g_wlog_n), &z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return (long long)n;
+}
+#endif

@@ -36,6 +36,7 @@ EXPORTED = [
     "spt_bvh_build_stats", "spt_scene_set_texture", "spt_scene_set_spheres", "spt_scene_set_material_kinds",
     "spt_scene_save", "spt_scene_load", "spt_scene_cache_info",
     "spt_scene_isect_busy_begin", "spt_scene_isect_busy_end", "spt_scene_kernel_busy",
+    "spt_debug_fail_workspace_alloc",
 ]
 SPT_MAT_DIFFUSE, SPT_MAT_MIRROR, SPT_MAT_GLASS = 0, 1, 2
 SPT_PIPELINE_AUTO, SPT_PIPELINE_WAVEFRONT, SPT_PIPELINE_FUSED = 0, 1, 2
@@ -96,7 +97,7 @@ class RenderStats(ctypes.Structure):
                 ("isect_begin_ms", c_double), ("isect_end_ms", c_double),
                 ("drained_paths", c_uint64), ("drain_launches", c_uint64), ("drained_casts", c_uint64),
                 ("drain_ms", c_double), ("drain_busy_ms", c_double), ("lockstep_casts", c_uint64),
-                ("fit_paths", c_uint64)]
+                ("fit_paths", c_uint64), ("fit_retries", c_uint64)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -178,6 +179,7 @@ def _load() -> ctypes.CDLL:
         "spt_last_error": (c_char_p, []),
         "spt_version": (c_char_p, []),
         "spt_build_id": (c_char_p, []),
+        "spt_debug_fail_workspace_alloc": (None, [ctypes.c_int32]),
         "spt_obj_load": (i32, [c_char_p, POINTER(Mesh)]),
         "spt_mesh_free": (None, [POINTER(Mesh)]),
         "spt_pbrt_load": (i32, [c_char_p, POINTER(Mesh), POINTER(PbrtInfo)]),

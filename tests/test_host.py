@@ -162,8 +162,8 @@ def test_config_defaults_and_env_overrides():
     assert (c.streams, c.isect_refill_idle, c.isect_static_share_q8, c.isect_chunk) == (4, 24, 128, 128)
     assert c.wavefront_paths == 1 << 25 and c.fused_max_paths == 1 << 20      # spt.h docs = code
     assert (c.drain_q8, c.drain_grid_q8, c.drain_casts) == (1024, 0, 1)
-    assert (c.fit_streams, c.fit_paths, c.sub_queues) == (2, 1 << 28, 1)
-    assert (c.drain_sort, c.lockstep_first, c.fit_chunks) == (0, 1, 1)
+    assert (c.fit_streams, c.fit_paths, c.sub_queues) == (1, 1 << 28, 1)
+    assert (c.drain_sort, c.lockstep_first, c.fit_chunks) == (0, 3, 1)
     assert sptamd.config_from_env(environ={"SPT_LOCKSTEP_FIRST": "0"}).lockstep_first == 0
     assert c.fit_bytes == 0 and sptamd.config_from_env(environ={"SPT_FIT_BYTES": "4096"}).fit_bytes == 4096
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
@@ -184,7 +184,7 @@ def test_config_defaults_and_env_overrides():
                                          ("bvh_width", 7), ("pack_groups", 3), ("work_order", 3),
                                          ("queue_cache", 3), ("drain_q8", 65536), ("drain_grid_q8", 4097),
                                          ("drain_casts", 65), ("fit_streams", 0), ("fit_streams", 5),
-                                         ("fit_paths", (1 << 31) + 1), ("lockstep_first", 2), ("fit_chunks", 2)])
+                                         ("fit_paths", (1 << 31) + 1), ("lockstep_first", 4), ("fit_chunks", 2)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)
