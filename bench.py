@@ -480,11 +480,20 @@ def main():
             # one-lane-per-ray kernel (spt_config.lockstep_first), later casts
             # and other jobs in the persistent one; the name says which ran
             lock = agg["lockstep_casts"]
-            isect_name = ("isect_lockstep_kernel" if lock == isect_casts else
-                          "isect_queue_kernel" if lock == 0 else "isect_lockstep_kernel+isect_queue_kernel")
+            # (lockstep_first >= 2 on a wide-BVH scene: the camera-cast kernel makes,
+            # traces and shades the first cast; it moves its survivors' queue
+            # entries and the others' film writes)
+            cam = scene.backend.config["lockstep_first"] >= 2 and int(sstats["bvh_width"]) != 2
+            first = "camera_cast_kernel" if cam else "isect_lockstep_kernel"
+            isect_name = (first if lock == isect_casts else
+                          "isect_queue_kernel" if lock == 0 else first + "+isect_queue_kernel")
+            kb = KERNEL_BYTES_PER_CAST
+            if cam and lock == isect_casts and isect_casts:
+                kb = round((agg["drained_paths"] * queue_b + (isect_casts - agg["drained_paths"]) * film_b)
+                           / isect_casts, 3)
             kernels[isect_name] = dict(
                 units=isect_casts, unit="ray cast", bytes_per_unit=ISECT_BYTES_PER_CAST,
-                kernel_bytes_per_unit=KERNEL_BYTES_PER_CAST, bytes=isect_casts * ISECT_BYTES_PER_CAST,
+                kernel_bytes_per_unit=kb, bytes=isect_casts * ISECT_BYTES_PER_CAST,
                 busy_ms=agg["isect_busy_ms"], launches=isect_launches, sum_ms=agg["isect_ms"], casts=isect_casts,
                 basis="algorithmic bytes of all isect launches / union of their intervals (isect busy)")
             if agg["drain_launches"]:
@@ -573,9 +582,10 @@ def main():
             "queue_cache_rule": "auto: non-temporal path-queue / hit accesses for scenes of >= 256 MiB, else "
                                 "cached (DESIGN.md §4)",
             "pipeline_rule": "auto: the wavefront (isect + ballot-compaction shade per cast; a job of <= 2^28 "
-                             "paths starts every path at once on two sub-wavefronts, a larger one in sample chunks "
-                             "that each do; the first cast in the one-lane-per-ray isect kernel; the drain finishes "
-                             "the paths still in flight after drain_casts casts; DESIGN.md §4, §6)"
+                             "paths starts every path at once on one sub-wavefront, a larger one in sample chunks "
+                             "that each do; the first cast in the camera-cast kernel (camera ray, lockstep trace and "
+                             "shade in one launch, survivors compacted per XCD shard); the drain finishes the paths "
+                             "still in flight after drain_casts casts; DESIGN.md §4, §6)"
                              if args.pipeline == "auto" else f"--pipeline {args.pipeline}",
             "config": {"pipeline": "fused" if fused else "wavefront", "streams": st.get("streams"),
                        "drain": None if fused else {
@@ -593,7 +603,12 @@ def main():
                        "triangles": int(sstats["ntri"]), "tiles": f"{world} x interleaved {R}-row groups",
                        "paths_in_flight": st.get("paths_in_flight"), "rays_per_path": round(s_bar, 4),
                        "work_order": work_order, "queue_cache": queue_cache},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            # the roof that binds: the larger of the HBM fraction (achieved / peak,
+            # kept as the headline frac so rounds stay comparable) and the VALU
+            # issue fraction of this build's PMC pass
+            "roofline": {"bound": "valu" if valu and valu["frac"] > achieved / HBM_PEAK_GBS else "hbm",
+                         "bound_rule": "the larger of frac (HBM bytes) and valu.frac (VALU issue, this build's PMC)",
+                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "kernel": dom_name,
                          "basis": dom["basis"],
@@ -603,9 +618,13 @@ def main():
                          "algorithmic_bytes_per_launch": round(bytes_per_launch),
                          "traffic_per_cast": traffic_per_unit,
                          "traffic_ratio": round(traffic / bytes_per_launch, 3) if traffic else None,
-                         "traffic_note": "HBM-side bytes per launch from the PMC passes (2 x FETCH_SIZE + WRITE_SIZE, "
-                                         "MI355X_MICROARCH.md gfx950 correction) of this build: node and triangle "
-                                         "gathers the caches miss, besides the algorithmic bytes",
+                         "traffic_note": "L2 memory-side bytes per launch from the PMC passes of this build "
+                                         "(FETCH_SIZE + WRITE_SIZE; FETCH_SIZE counts the traversal's random 64-B "
+                                         "node / triangle gathers exactly, profiles/r06_fetch_calibration/; "
+                                         "traffic_hi_per_cast doubles the reads, the bound for coalesced 128-B "
+                                         "requests): node and triangle gathers the caches miss, besides the "
+                                         "algorithmic bytes",
+                         "traffic_hi_per_cast": pmc.get("traffic_hi_bytes_per_cast") if pmc else None,
                          "busy_ms_per_step": round(busy_ms / args.steps, 4),
                          "busy_note": "union over the step's launch intervals and over consecutive steps' renders, "
                                       "which overlap on two streams",

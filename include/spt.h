@@ -465,16 +465,18 @@ spt_status spt_hit_info_compute(spt_scene scene, const spt_rays* rays, const spt
  * device buffer of 3 x tile_rows x width floats (planar R, G, B as the
  * reference's SpectrumC film, main.cpp:369), already divided by spp.  The
  * call returns after the stream has drained.  stats may be NULL.
- * Threading: a scene owns one render workspace (path queues, film chunks,
- * events), so spt_render calls on one scene are serialised by a per-scene
- * mutex (a second thread waits); render concurrently from one scene per
- * thread / device.  spt_scene_set_config and the other scene setters
- * (albedo, emission, textures, spheres, material kinds) take the same mutex;
- * spt_intersect / spt_hit_info_compute take it only to snapshot the scene's
- * device arrays and knobs before their (asynchronous) launch.  A setter that
- * replaces device arrays frees the old ones, so it must not run while a
- * launch that read them is still in flight on some stream: synchronise
- * first. */
+ * Threading: every call on a scene holds a per-scene mutex while it enqueues
+ * (a second thread waits); render concurrently from one scene per thread /
+ * device.  spt_intersect and spt_hit_info_compute launch while holding it and
+ * record an event on their stream.  The scene setters (albedo, emission,
+ * textures, spheres, material kinds) and spt_scene_destroy block the host
+ * until every queued render of the scene and the last public call on every
+ * stream have finished before they free or replace a device array, so a
+ * launch already queued always reads the state it was queued with; no caller
+ * synchronisation is needed (spt_scene_set_config changes only knobs the
+ * next call reads).  A render does not run on `stream` itself: it runs on its
+ * working set's own streams (below), after `stream`'s prior work (an event),
+ * and `stream`'s next work waits for the render's end (an event). */
 spt_status spt_render(spt_scene scene, const spt_render_params* params, float* film_dev,
                       spt_render_stats* stats, void* stream);
 
@@ -493,7 +495,14 @@ spt_status spt_render(spt_scene scene, const spt_render_params* params, float* f
  * spt_render_wait.  A scene keeps two working sets (queues, film chunk,
  * sub-wavefront streams), each bound to the caller stream it was first used
  * with: renders queued alternately on two streams overlap (one drains while
- * the next starts); a third stream takes over the least recently used set. */
+ * the next starts); a third stream takes over the least recently used set.
+ * A set's streams are created with a full CU mask (spt_config.sub_queues),
+ * which gives each a hardware queue of its own; such streams are blocking
+ * streams, so legacy null-stream work serialises with them.  A set bound to
+ * the legacy null stream (or the per-thread default stream) therefore uses
+ * plain non-blocking streams and runs a fitting job on one sub-wavefront.
+ * For overlapping renders, queue them on two streams of your own that have
+ * hardware queues of their own. */
 spt_status spt_render_async(spt_scene scene, const spt_render_params* params, float* film_dev, void* stream,
                             uint64_t* ticket);
 spt_status spt_render_wait(spt_scene scene, uint64_t ticket, spt_render_stats* stats);

@@ -497,7 +497,7 @@ hipError_t ws_malloc(void** p, size_t bytes) {
 }
 
 spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uint32_t planes, size_t film_bytes,
-                            size_t acc_floats, bool own_queues) {
+                            size_t acc_floats, bool own_queues, bool drain_sort) {
     bool quiet = !ws.used;
     const auto quiesce = [&]() -> spt_status {
         if (!quiet) HIP_TRY(hipEventSynchronize(ws.free_ev));
@@ -517,6 +517,21 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
             b.cap = cap;
             b.pad = pad;
             b.planes = planes;
+        }
+        // spt_config.drain_sort: the forced drain's sort keys / values and hipcub
+        // scratch over cap slots, allocated here, where the set is quiesced
+        // (not in the middle of an enqueue, behind a host sync)
+        if (drain_sort && b.sort_cap < b.cap) {
+            if ((st = quiesce())) return st;
+            hfree(b.sort_buf);
+            if (b.sort_tmp) (void)hipFree(b.sort_tmp);
+            b.sort_tmp = nullptr;
+            b.sort_cap = 0;
+            HIP_TRY(ws_malloc((void**)&b.sort_buf, sizeof(uint32_t) * 4 * b.cap));
+            HIP_TRY(launch_drain_sort(DeviceScene{}, PathQueue{}, nullptr, (uint32_t)b.cap, nullptr, nullptr, nullptr,
+                                      nullptr, nullptr, &b.sort_tmp_bytes, nullptr));
+            HIP_TRY(ws_malloc(&b.sort_tmp, std::max<size_t>(b.sort_tmp_bytes, 16)));
+            b.sort_cap = b.cap;
         }
         if (!b.cnt) HIP_TRY(ws_malloc((void**)&b.cnt, sizeof(Counters)));
         if (!b.host_cnt) HIP_TRY(hipHostMalloc((void**)&b.host_cnt, 2 * sizeof(Counters), hipHostMallocDefault));
@@ -560,9 +575,12 @@ spt_status ensure_workspace(WorkSet& ws, int nsub, size_t cap, uint32_t pad, uin
 spt_status release_queues(WorkSet& ws) {
     if (ws.used) HIP_TRY(hipEventSynchronize(ws.free_ev));
     for (Sub& b : ws.sub) {
-        hfree(b.qa); hfree(b.qb); hfree(b.hits);
+        hfree(b.qa); hfree(b.qb); hfree(b.hits); hfree(b.sort_buf);
+        if (b.sort_tmp) (void)hipFree(b.sort_tmp);
+        b.sort_tmp = nullptr;
         b.cap = 0;
         b.planes = 0;
+        b.sort_cap = 0;
     }
     hfree(ws.film);
     ws.film_cap = 0;
@@ -2108,7 +2126,7 @@ retry_fit:
     WorkSet& ws = sc->ws.pick_set(caller);
     ws.last_ticket = sc->ws.next_ticket;
     st = ensure_workspace(ws, K, Ck, cfg.plane_pad, mode_planes(mode), (size_t)chunk * film_unit * P, 3 * P,
-                          own_queues);
+                          own_queues, !fused && cfg.drain_q8 != 0 && cfg.drain_sort != 0 && sc->nodes8 != nullptr);
     if (st == SPT_ERR_OOM && !fused && C > kMinRetryPaths) {
         // the fit, or below it the per-cast wavefront and its film chunk, halved;
         // first the queues, hit records and film chunk this attempt allocated
@@ -2493,19 +2511,7 @@ retry_fit:
                         da[k].drain_below = 0xffffffffu;
                         da[k].perm = nullptr;
                         if (drain_sort) {  // the drain's order: by direction octant, then origin (kernels.hip)
-                            const size_t cap = b.cap;
-                            if (b.sort_cap < cap) {
-                                HIP_TRY(hipStreamSynchronize(strm[k]));  // a previous render may still sort in them
-                                hfree(b.sort_buf);
-                                if (b.sort_tmp) (void)hipFree(b.sort_tmp);
-                                b.sort_tmp = nullptr;
-                                b.sort_cap = 0;
-                                HIP_TRY(hipMalloc((void**)&b.sort_buf, sizeof(uint32_t) * 4 * cap));
-                                HIP_TRY(launch_drain_sort(sc->dev(), q[k][c], nullptr, (uint32_t)cap, nullptr, nullptr,
-                                                          nullptr, nullptr, nullptr, &b.sort_tmp_bytes, strm[k]));
-                                HIP_TRY(hipMalloc(&b.sort_tmp, std::max<size_t>(b.sort_tmp_bytes, 16)));
-                                b.sort_cap = cap;
-                            }
+                            const size_t cap = b.cap;  // (buffers: ensure_workspace)
                             uint32_t* kb = b.sort_buf;
                             HIP_TRY(launch_drain_sort(sc->dev(), q[k][c], &b.cnt->qn[c], (uint32_t)b.cap, kb, kb + cap,
                                                       kb + 2 * cap, kb + 3 * cap, b.sort_tmp, &b.sort_tmp_bytes,

@@ -8,11 +8,16 @@ Each CSV is one pass (run_counter_collection.csv).  Every counter is averaged
 over the isect dispatches of its pass.  BENCH_LOG holds the bench JSON line of
 one pass (casts per launch = algorithmic bytes per launch / bytes per cast).
 Derived, per launch and per ray cast:
-  traffic = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B).  gfx950 correction from
-      MI355X_MICROARCH.md §HBM: FETCH_SIZE reads half the bytes of a wide
-      coalesced stream, so reads are doubled; it also counts Infinity-Cache
-      hits, and the guide calibrates the correction for 16 B/lane streams
-      only, so for the scattered node gathers it is an estimate.
+  traffic = FETCH_SIZE + WRITE_SIZE (KiB -> B).  Calibrated for this access
+      pattern (profiles/r06_fetch_calibration/, tools/micro_fetch.hip):
+      FETCH_SIZE = memory-side read requests x 64 B; a random 64-B gather —
+      a node visit (4 x 16 B of one 64-B node) or a triangle record (3 x 12 B
+      of one 64-B record) — is one 64-B request, counted exactly (factor
+      1.00 / 0.94 against the true bytes), while a 128-B line or a coalesced
+      stream is one 128-B request counted at 64 B (factor 2, the
+      MI355X_MICROARCH.md correction).  The traversal's misses are the 64-B
+      gathers, so reads count x1; traffic_hi (reads x2) bounds the share of
+      coalesced queue reads.  FETCH_SIZE also counts Infinity-Cache hits.
   valu_insts = SQ_INSTS_VALU (wave64 VALU instructions, all waves).
   l2_hit_rate = TCC_HIT / (TCC_HIT + TCC_MISS).
 The result is merged into OUT_JSON under KEY (e.g. "config1"); bench.py reads
@@ -85,14 +90,19 @@ def main(out, key, log, *paths):
     if cast_per_launch:
         rec["casts_per_launch"] = cast_per_launch
     if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
-        t = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
+        t = (mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
+        t_hi = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
         rec["traffic_bytes_per_launch"] = t
         rec[f"traffic_bytes_per_{unit}"] = t / casts
+        rec[f"traffic_hi_bytes_per_{unit}"] = t_hi / casts
         if cast_per_launch and unit != "cast":
             rec["traffic_bytes_per_cast"] = t / cast_per_launch
-        rec[f"read_bytes_per_{unit}"] = 2.0 * mean["FETCH_SIZE"] * 1024.0 / casts
+            rec["traffic_hi_bytes_per_cast"] = t_hi / cast_per_launch
+        rec[f"read_bytes_per_{unit}"] = mean["FETCH_SIZE"] * 1024.0 / casts
         rec[f"write_bytes_per_{unit}"] = mean["WRITE_SIZE"] * 1024.0 / casts
-        rec["traffic_correction"] = "reads x2 (gfx950 FETCH_SIZE half-count, MI355X_MICROARCH.md HBM); estimate"
+        rec["traffic_correction"] = ("reads x1: FETCH_SIZE counts a random 64-B gather (node, triangle record) "
+                                     "exactly, profiles/r06_fetch_calibration/; traffic_hi: reads x2 (coalesced "
+                                     "128-B requests, MI355X_MICROARCH.md)")
     if "SQ_INSTS_VALU" in mean:
         rec["valu_insts_per_launch"] = mean["SQ_INSTS_VALU"]
         rec[f"valu_insts_per_{unit}"] = mean["SQ_INSTS_VALU"] / casts
