@@ -344,6 +344,10 @@ typedef struct spt_config {
                                        scenes sharing the GPU); an allocation that fails anyway
                                        halves the fit and retries.  The image does not depend on
                                        it                                                      */
+    uint32_t drain_refill_idle;     /* the drain's lane loop refills (and shades) once this many of a
+                                       wave's lanes are idle, 24 (the fused kernel keeps
+                                       fused_refill_idle, 32: config 1 +1.8 % at 24 in the drain,
+                                       the fused kernel -2.5 %)              [1..64] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

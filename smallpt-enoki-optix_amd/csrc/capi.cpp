@@ -809,6 +809,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(drain_sort, 0, 1)
     CFG_RANGE(lockstep_first, 0, 3)
     CFG_RANGE(fit_chunks, 0, 1)
+    CFG_RANGE(drain_refill_idle, 1, 64)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -1208,6 +1209,7 @@ void spt_default_config(spt_config* c) {
     c->drain_grid_q8 = 0;
     c->drain_casts = kDefaultDrainCasts;
     c->fit_streams = 1;
+    c->drain_refill_idle = 24;
     c->fit_paths = kDefaultFitPaths;
     c->sub_queues = 1;
     c->drain_sort = 0;
@@ -2326,7 +2328,7 @@ retry_fit:
             D.P = (uint32_t)P; D.W = p.width; D.max_depth = p.max_depth;
             D.rr_start = p.rr_start_depth; D.rng_order = p.rng_order;
             D.tile_index = p.tile_index; D.tile_count = p.tile_count; D.rows_per_group = p.rows_per_group;
-            D.refill_idle = cfg.fused_refill_idle;
+            D.refill_idle = cfg.drain_refill_idle;
             D.static_share_q8 = cfg.fused_static_share_q8;
             D.chunk = cfg.isect_chunk;
             D.grid_q8 = cfg.drain_grid_q8 ? cfg.drain_grid_q8 : 256u / (uint32_t)K;

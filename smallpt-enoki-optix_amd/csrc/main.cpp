@@ -10,8 +10,9 @@
 // of the scene (replicated BVH) and renders its interleaved row-group tile
 // (spt_render_params.tile_*), then ONE RCCL collective, ncclGather over xGMI
 // from a communicator per device (ncclCommInitAll, driven from one thread in
-// an ncclGroupStart/End), brings the fp32 tiles to device 0, whose rows are
-// put back in place.  Pixel RNG streams are keyed by the global pixel, so
+// an ncclGroupStart/End), queued on each rank's stream behind its render
+// (spt_render_async, no host synchronisation between them), brings the fp32
+// tiles to device 0, whose rows are put back in place.  Pixel RNG streams are keyed by the global pixel, so
 // the image is bit-identical for any N.  --rehearse-shared-gpu places every
 // tile on device 0 and gathers with device copies instead (a one-GPU box
 // cannot host two RCCL ranks), so the tiling and assembly run anywhere.
@@ -57,6 +58,8 @@ struct Rank {
     std::vector<uint32_t> rows;   // this tile's image rows (spt_tile_rows)
     float* tile = nullptr;        // (3, max_rows, W) fp32, padded to the largest tile
     hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;    // recorded on `stream` behind the queued render
+    uint64_t ticket = 0;          // spt_render_async's, collected after the gather
     spt_render_stats st{};
     std::exception_ptr err;
 };
@@ -103,6 +106,7 @@ void render_multi(const std::string& path, const spt::Mesh* mesh, spt_render_par
         if (mesh) k.scene.commit_from(*mesh, k.device);
         else k.scene.load(path, k.device);
         hip_check(hipStreamCreateWithFlags(&k.stream, hipStreamNonBlocking), "hipStreamCreate");
+        hip_check(hipEventCreateWithFlags(&k.done, hipEventDisableTiming), "hipEventCreate");
         hip_check(hipMalloc((void**)&k.tile, sizeof(float) * count), "hipMalloc tile");
         hip_check(hipMemsetAsync(k.tile, 0, sizeof(float) * count, k.stream), "hipMemset tile");
         hip_check(hipStreamSynchronize(k.stream), "hipStreamSynchronize");
@@ -119,13 +123,17 @@ void render_multi(const std::string& path, const spt::Mesh* mesh, spt_render_par
     hip_check(hipMalloc((void**)&recv, sizeof(float) * count * ngpu), "hipMalloc gather");
 
     const auto t0 = clock_t_::now();
-    each([&](Rank& k) {  // every rank renders its tile (main.cpp:385-429 on its rows)
+    // every rank queues its tile's render (main.cpp:385-429 on its rows) on its
+    // stream and returns: the gather below is queued on the same streams behind
+    // the renders (spt_render_async: the caller stream's next work waits for
+    // the render), so no host synchronisation sits between render and gather
+    each([&](Rank& k) {
         spt_render_params q = p;
         q.tile_index = (uint32_t)k.index;
         q.tile_count = (uint32_t)ngpu;
         q.rows_per_group = rows_per_group;
-        if (!k.rows.empty()) k.scene.render(q, k.tile, &k.st, k.stream);
-        hip_check(hipStreamSynchronize(k.stream), "hipStreamSynchronize");
+        if (!k.rows.empty()) k.ticket = k.scene.render_async(q, k.tile, k.stream);
+        hip_check(hipEventRecord(k.done, k.stream), "hipEventRecord");
     });
     // the one exchange step: the fp32 tiles to device 0
     if (!shared) {
@@ -143,13 +151,19 @@ void render_multi(const std::string& path, const spt::Mesh* mesh, spt_render_par
         }
     } else {
         hip_check(hipSetDevice(ranks[0]->device), "hipSetDevice");
-        for (int r = 0; r < ngpu; r++)
+        for (int r = 0; r < ngpu; r++) {
+            // (device copies on rank 0's stream, each behind that rank's render)
+            hip_check(hipStreamWaitEvent(ranks[0]->stream, ranks[r]->done, 0), "hipStreamWaitEvent");
             hip_check(hipMemcpyAsync(recv + (size_t)r * count, ranks[r]->tile, sizeof(float) * count,
                                      hipMemcpyDeviceToDevice, ranks[0]->stream),
                       "hipMemcpy gather");
+        }
         hip_check(hipStreamSynchronize(ranks[0]->stream), "hipStreamSynchronize");
     }
     ms = ms_since(t0);
+    each([&](Rank& k) {  // the renders' statistics (their work is done: the gather waited for it)
+        if (!k.rows.empty()) k.scene.render_wait(k.ticket, &k.st);
+    });
 
     // rank 0 puts every tile's rows back in place
     std::vector<float> gathered(count * ngpu);
@@ -172,6 +186,7 @@ void render_multi(const std::string& path, const spt::Mesh* mesh, spt_render_par
     for (auto& k : ranks) {
         hip_check(hipSetDevice(k->device), "hipSetDevice");
         (void)hipFree(k->tile);
+        (void)hipEventDestroy(k->done);
         (void)hipStreamDestroy(k->stream);
     }
 }

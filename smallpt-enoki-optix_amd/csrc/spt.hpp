@@ -72,6 +72,16 @@ class Scene {
         if (n != 0 && n != sizeof(pbrt_)) throw std::runtime_error(path + ": extra bytes are not an spt_pbrt_info");
         if (n == 0) pbrt_ = spt_pbrt_info{};
     }
+    // spt_render_async / spt_render_wait: queue the render on `stream` (the
+    // stream's next work waits for it) and collect its statistics later
+    uint64_t render_async(const spt_render_params& p, float* film_dev, void* stream) {
+        uint64_t ticket = 0;
+        check(spt_render_async(scene_, &p, film_dev, stream, &ticket), "spt_render_async");
+        return ticket;
+    }
+    void render_wait(uint64_t ticket, spt_render_stats* stats) {
+        check(spt_render_wait(scene_, ticket, stats), "spt_render_wait");
+    }
     void render(const spt_render_params& p, float* film_dev, spt_render_stats* stats, void* stream = nullptr) {
         check(spt_render(scene_, &p, film_dev, stats, stream), "spt_render");
     }

@@ -127,7 +127,7 @@ class Config(ctypes.Structure):
                 ("drain_q8", c_uint32), ("drain_grid_q8", c_uint32), ("drain_casts", c_uint32),
                 ("fit_streams", c_uint32), ("fit_paths", c_uint64), ("sub_queues", c_uint32),
                 ("drain_sort", c_uint32), ("lockstep_first", c_uint32), ("fit_chunks", c_uint32),
-                ("fit_bytes", c_uint64)]
+                ("fit_bytes", c_uint64), ("drain_refill_idle", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -262,6 +262,7 @@ _ENV_CONFIG = {
     "SPT_LOCKSTEP_FIRST": ("lockstep_first", int),
     "SPT_FIT_CHUNKS": ("fit_chunks", int),
     "SPT_FIT_BYTES": ("fit_bytes", int),
+    "SPT_DRAIN_IDLE": ("drain_refill_idle", int),
 }
 
 
