@@ -1152,6 +1152,9 @@ __global__ __launch_bounds__(256) void refill_kernel(RefillArgs a) {
 }
 
 // ----------------------------------------------------------------- shade
+#ifndef SPT_OCT_GROUP
+#define SPT_OCT_GROUP 0
+#endif
 // main.cpp:404-425 for one cast of every queued path.  A path that ends
 // writes its contribution once per (sample, pixel): unit mode one byte
 // (escaped or not: the sky term is added in sample order by the resolve),
@@ -1358,7 +1361,27 @@ __device__ __forceinline__ void shade_block(const ShadeArgs& a, bool valid, cons
         }
     }
     __syncthreads();
-    if (emit) store_path<kMode, kNt>(a.out, s_wave_off[wave] + rank, no, nd, pix, meta + 1u, tr, tg, tb, lr, lg, lb);
+    uint32_t slot_in_wave = rank;
+#if SPT_OCT_GROUP
+    // a wave's survivors in the order of their bounce direction's octant (then
+    // lane order): the drain's lanes take consecutive queue entries, so rays
+    // refilled together start out heading the same way (order only: the same
+    // paths, the same bits)
+    {
+        const uint32_t oct = emit ? (nd.x < 0.0f ? 1u : 0u) | (nd.y < 0.0f ? 2u : 0u) | (nd.z < 0.0f ? 4u : 0u) : 8u;
+        uint32_t before = 0, mine = 0;
+#pragma unroll
+        for (uint32_t o = 0; o < 8u; o++) {
+            const uint64_t b = __ballot(oct == o);
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            if (oct == o) mine = before + r;
+            before += (uint32_t)__popcll(b);
+        }
+        slot_in_wave = mine;
+    }
+#endif
+    if (emit)
+        store_path<kMode, kNt>(a.out, s_wave_off[wave] + slot_in_wave, no, nd, pix, meta + 1u, tr, tg, tb, lr, lg, lb);
 }
 
 template <int kMode, bool kSpt, bool kNt = false>
@@ -1476,7 +1499,12 @@ void render_fused_kernel(FusedArgs a) {
             n = wave_uniform(*a.qcount);
         }
         if (n >= a.drain_below) return;  // the isect and shade launches take this queue
-        if (blockIdx.x == 0 && threadIdx.x == 0 && n) atomicAdd(a.drained, (unsigned long long)n);
+        if (blockIdx.x == 0 && threadIdx.x == 0 && n) {
+            atomicAdd(a.drained, (unsigned long long)n);
+            // a forced drain ends its sub-wavefront: the queued paths' first casts
+            // here go to the stats directly (no bookkeeping refill follows)
+            if (a.count_queue) atomicAdd(&a.stats[0], (unsigned long long)n);
+        }
     }
     NoStats st;
     Tr tr;

@@ -411,6 +411,8 @@ struct FusedArgs {
     // seg_count[j * kShardStride] paths first, then steal; no static share.
     const uint32_t* seg_count;
     uint32_t seg_items, seg_block;
+    uint32_t count_queue;           // 1: add the queue's paths (their casts here) to stats[0] (a forced
+                                    // drain, which no bookkeeping refill follows)
 };
 
 struct HitInfoArgs {
