@@ -32,7 +32,7 @@ import sys
 from collections import defaultdict
 
 
-def passes(paths, kernel=r"isect_(queue|lockstep)"):
+def passes(paths, kernel=r"isect_(queue|lockstep)|camera_cast"):
     per = defaultdict(dict)  # counter -> {dispatch: value}
     for path in paths:
         fh = gzip.open(path, "rt") if path.endswith(".gz") else open(path)  # committed passes are gzipped
@@ -53,7 +53,7 @@ def bench_line(log):
 
 
 def main(out, key, log, *paths):
-    kernel = r"isect_(queue|lockstep)"
+    kernel = r"isect_(queue|lockstep)|camera_cast"
     paths = list(paths)
     if "--kernel" in paths:
         i = paths.index("--kernel")

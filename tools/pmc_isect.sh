@@ -9,7 +9,7 @@ set -u
 out=${1:-gpurun_out/pmc}
 cfg=${CONFIG:-1}
 pipe=${PIPE:-auto}
-regex='isect_(queue|lockstep)'
+regex='isect_(queue|lockstep)|camera_cast'
 key=config$cfg
 if [ "$pipe" = fused ]; then regex=render_fused; key=config${cfg}_fused; fi
 # KERNEL=drain: the wavefront's drain (render_fused_kernel<drain>), key "config<N>_drain"
