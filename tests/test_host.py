@@ -232,3 +232,22 @@ def test_env_snapshot_tracks_environment(monkeypatch):
     monkeypatch.setenv("SPT_STREAMS", "")
     assert _lib.config_from_env().streams == _lib.default_config().streams
     assert _lib.env_snapshot({"SPT_STREAMS": "2"})[i] == "2"
+
+
+def test_shard_base_partitions_items(tmp_path):
+    """The sharded camera cast's queue segments (spt_internal.h shard_base):
+    for every item count and block size, segment j starts where shards 0..j-1's
+    threads end, and the eight segments cover exactly the items (the drain's
+    per-XCD pools read them by the same formula)."""
+    import shutil
+    import subprocess
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(os.path.dirname(__file__), "native", "shard_base_check.cpp")
+    exe = tmp_path / "shard_base_check"
+    csrc = os.path.join(os.path.dirname(os.path.dirname(__file__)), "smallpt-enoki-optix_amd", "csrc")
+    subprocess.run([hipcc, "-std=c++17", "-I" + csrc, "-x", "hip", "--offload-arch=gfx950", "-o", str(exe), src],
+                   check=True, capture_output=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    assert '"bad": 0' in out, out
