@@ -592,7 +592,11 @@ def main():
                            "drained_paths_per_step": round(agg["drained_paths"] / args.steps),
                            "drained_casts_per_step": round(agg["drained_casts"] / args.steps),
                            "wavefront_casts_per_step": round((agg["ray_casts"] - agg["drained_casts"]) / args.steps),
-                           "drain_launches_per_step": round(agg["drain_launches"] / args.steps, 2)},
+                           "drain_launches_per_step": round(agg["drain_launches"] / args.steps, 2),
+                           "refill_idle": st.get("drain_refill_idle"),
+                           "refill_idle_rule": "auto (drain_refill_idle 0): 56 for scenes of <= 1024 triangles, "
+                                               "40 when the queue is streamed, else 24 (DESIGN.md §4)"
+                                               if scene.backend.config["drain_refill_idle"] == 0 else "set"},
                        "hw_queues": {"in_effect": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),
                                      "environment": HW_QUEUES_ENV,
                                      "note": "the environment's GPU_MAX_HW_QUEUES (SPT_HW_QUEUES overrides it for "

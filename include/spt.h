@@ -151,6 +151,8 @@ typedef struct spt_render_stats {
                                    queues would not fit in device memory (spt_config.fit_bytes) */
     uint64_t fit_retries;       /* working-set allocations that failed and were retried with half
                                    the paths in flight (device memory taken by someone else) */
+    uint32_t drain_refill_idle; /* wavefront: the drain's refill threshold that ran
+                                   (spt_config.drain_refill_idle or its AUTO choice; 0: no drain) */
 } spt_render_stats;
 
 typedef struct spt_scene_stats {
@@ -345,9 +347,12 @@ typedef struct spt_config {
                                        halves the fit and retries.  The image does not depend on
                                        it                                                      */
     uint32_t drain_refill_idle;     /* the drain's lane loop refills (and shades) once this many of a
-                                       wave's lanes are idle, 24 (the fused kernel keeps
-                                       fused_refill_idle, 32: config 1 +1.8 % at 24 in the drain,
-                                       the fused kernel -2.5 %)              [1..64] */
+                                       wave's lanes are idle.  0 = AUTO: 56 for scenes of at most
+                                       1024 triangles (a trace step is cheap next to a refill:
+                                       config 2 +20 % over 24), 40 when the queue is streamed
+                                       (queue_cache; config 4 +3 %), else 24 (config 1 +1.8 %
+                                       over 32).  The fused kernel keeps fused_refill_idle.
+                                       The image does not depend on it   [0..64] */
 } spt_config;
 
 void spt_default_config(spt_config* cfg);

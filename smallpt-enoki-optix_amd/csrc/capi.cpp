@@ -809,7 +809,7 @@ spt_status check_config(const spt_config& c) {
     CFG_RANGE(drain_sort, 0, 1)
     CFG_RANGE(lockstep_first, 0, 3)
     CFG_RANGE(fit_chunks, 0, 1)
-    CFG_RANGE(drain_refill_idle, 1, 64)
+    CFG_RANGE(drain_refill_idle, 0, 64)
 #undef CFG_RANGE
     return SPT_OK;
 }
@@ -1209,7 +1209,7 @@ void spt_default_config(spt_config* c) {
     c->drain_grid_q8 = 0;
     c->drain_casts = kDefaultDrainCasts;
     c->fit_streams = 1;
-    c->drain_refill_idle = 24;
+    c->drain_refill_idle = 0;
     c->fit_paths = kDefaultFitPaths;
     c->sub_queues = 1;
     c->drain_sort = 0;
@@ -2092,6 +2092,19 @@ retry_fit:
     const uint32_t queue_nt =
         cfg.queue_cache == SPT_QUEUE_CACHE_STREAM ||
         (cfg.queue_cache == SPT_QUEUE_CACHE_AUTO && scene_bytes >= kPixelMajorMinSceneBytes);
+    // The drain's refill threshold (spt_config.drain_refill_idle).  AUTO: a
+    // wave refills and shades once per batch of free lanes, at a cost that
+    // does not depend on how many lanes take part, while a trace step costs
+    // in proportion to how long its busiest lane traverses.  A scene of a few
+    // triangles (smallpt's walls: the spheres are tested in the shade) traces
+    // in a step or two, so batching more lanes pays (config 2: 56 +20 % over
+    // 24); a scene beyond the Infinity Cache (config 4) +3 % at 40; the
+    // cache-resident mitsuba mesh -2 % at 32 (configs 1, 3), while the
+    // tessellated Cornell spheres (75k triangles) gain 1-6 % at 40: the rule
+    // keys on what the benchmarks separate (profiles/r06_exp/refill_idle/).
+    const uint32_t drain_idle = cfg.drain_refill_idle ? cfg.drain_refill_idle
+                                : sc->ntri <= kTraceLightTris ? kDrainIdleTraceLight
+                                : queue_nt ? kDrainIdleStream : kDrainIdleCached;
     if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
         C = kPixelMajorWavefrontPaths;
     if (fit) C = fit_chunk ? (uint64_t)fit_chunk * P : P * p.spp;
@@ -2328,7 +2341,7 @@ retry_fit:
             D.P = (uint32_t)P; D.W = p.width; D.max_depth = p.max_depth;
             D.rr_start = p.rr_start_depth; D.rng_order = p.rng_order;
             D.tile_index = p.tile_index; D.tile_count = p.tile_count; D.rows_per_group = p.rows_per_group;
-            D.refill_idle = cfg.drain_refill_idle;
+            D.refill_idle = drain_idle;
             D.static_share_q8 = cfg.fused_static_share_q8;
             D.chunk = cfg.isect_chunk;
             D.grid_q8 = cfg.drain_grid_q8 ? cfg.drain_grid_q8 : 256u / (uint32_t)K;
@@ -2685,6 +2698,7 @@ retry_fit:
     rs.queue_cache = fused ? 0u : (queue_nt && !trav_stats ? SPT_QUEUE_CACHE_STREAM : SPT_QUEUE_CACHE_CACHED);
     rs.streams = (uint32_t)K;
     rs.fused = fused ? 1u : 0u;
+    rs.drain_refill_idle = !fused && drain_on ? drain_idle : 0u;
     slot->regen_base = std::min<uint64_t>(C, P * p.spp);
     slot->ticket = sc->ws.next_ticket++;
     slot->pending = true;

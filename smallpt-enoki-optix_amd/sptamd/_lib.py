@@ -97,7 +97,8 @@ class RenderStats(ctypes.Structure):
                 ("isect_begin_ms", c_double), ("isect_end_ms", c_double),
                 ("drained_paths", c_uint64), ("drain_launches", c_uint64), ("drained_casts", c_uint64),
                 ("drain_ms", c_double), ("drain_busy_ms", c_double), ("lockstep_casts", c_uint64),
-                ("fit_paths", c_uint64), ("fit_retries", c_uint64)]
+                ("fit_paths", c_uint64), ("fit_retries", c_uint64),
+                ("drain_refill_idle", c_uint32)]
 
     def as_dict(self) -> dict:
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -312,3 +312,26 @@ def test_xcd_pools_bitexact(mesh, mode, lockstep, w, h, monkeypatch):
         np.testing.assert_array_equal(film.cpu().numpy(), ref)
         assert st["ray_casts"] == casts
         assert_work_complete(st, h, w, SPP)
+
+
+@pytest.mark.parametrize("mode", ["unit", "emit_spheres"])
+@pytest.mark.parametrize("idle", [0, 1, 40, 64])
+def test_drain_refill_idle_bitexact(mesh, mode, idle, monkeypatch):
+    """spt_config.drain_refill_idle: the drain's refill threshold (AUTO: 24 for
+    this cache-resident mesh of more than 1024 triangles, 40 with the queue
+    streamed) only reorders the drain's work — same bits, same casts."""
+    for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
+        monkeypatch.delenv(k)
+    mat = materials(mesh, mode)
+    kw = dict(rr_start_depth=3, env=(1.0, 0.9, 0.8))
+    osc = O.OracleScene(mesh, albedo=mat.get("albedo"), emission=mat.get("emission"), spheres=mat.get("spheres"),
+                        sphere_mat=mat.get("sphere_mat"), kinds=mat.get("kinds"))
+    ref, casts = osc.render(O.reference_params(W, H, SPP, D, **kw))
+    for cache in (sptamd._lib.SPT_QUEUE_CACHE_AUTO, sptamd._lib.SPT_QUEUE_CACHE_STREAM):
+        s = gpu_scene(mesh, mat, drain_refill_idle=idle, queue_cache=cache)
+        film, st = s.render(sptamd.make_params(W, H, SPP, D, pipeline="wavefront", **kw), stream=torch.cuda.Stream())
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(film.cpu().numpy(), ref)
+        assert st["ray_casts"] == casts and st["drained_paths"] > 0
+        auto = 40 if cache == sptamd._lib.SPT_QUEUE_CACHE_STREAM else 24
+        assert st["drain_refill_idle"] == (idle or auto)

@@ -21,9 +21,9 @@ def mesh():
     return scenes.smallpt_analytic(detail=0.5)
 
 
-def gscene(mesh, **over):
+def gscene(mesh, config=None, **over):
     m = dict(mesh, **over)
-    s = sptamd.Scene()
+    s = sptamd.Scene(config=config)
     s.add_arrays(m)
     s.commit(0)
     alb, emi = scenes.smallpt_materials(m)
@@ -54,6 +54,22 @@ def test_smallpt_scene_bitexact(mesh, pipeline, rr):
     np.testing.assert_array_equal(got, ref)
     assert st["ray_casts"] == casts
     assert ref.mean() > 0.05          # the light sphere is seen
+
+
+@pytest.mark.parametrize("idle", [0, 1, 24, 64])
+def test_smallpt_drain_refill_idle(mesh, idle, monkeypatch):
+    """spt_config.drain_refill_idle on smallpt's scene (a few wall triangles:
+    AUTO picks 56): when a drain wave refills changes only the
+    order of the work, not the bits."""
+    monkeypatch.delenv("SPT_DRAIN_IDLE", raising=False)
+    cfg = sptamd.default_config()
+    cfg.drain_refill_idle = idle
+    kw = dict(rr_start_depth=3, env=(0.0, 0.0, 0.0))
+    got, st = render(gscene(mesh, config=cfg), 64, 48, 8, 8, pipeline="wavefront", **kw)
+    ref, casts = oracle_render(mesh, 64, 48, 8, 8, **kw)
+    np.testing.assert_array_equal(got, ref)
+    assert st["ray_casts"] == casts and st["drained_paths"] > 0
+    assert st["drain_refill_idle"] == (idle or 56)
 
 
 def test_spheres_diffuse_and_sky_small_queue(mesh):

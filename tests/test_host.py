@@ -166,7 +166,7 @@ def test_config_defaults_and_env_overrides():
     assert (c.drain_sort, c.lockstep_first, c.fit_chunks) == (0, 3, 1)
     assert sptamd.config_from_env(environ={"SPT_LOCKSTEP_FIRST": "0"}).lockstep_first == 0
     assert c.fit_bytes == 0 and sptamd.config_from_env(environ={"SPT_FIT_BYTES": "4096"}).fit_bytes == 4096
-    assert c.drain_refill_idle == 24 and sptamd.config_from_env(environ={"SPT_DRAIN_IDLE": "40"}).drain_refill_idle == 40
+    assert c.drain_refill_idle == 0 and sptamd.config_from_env(environ={"SPT_DRAIN_IDLE": "40"}).drain_refill_idle == 40
     d = sptamd.config_from_env(environ={"SPT_DRAIN_Q8": "0", "SPT_DRAIN_CASTS": "4", "SPT_FIT_PATHS": "0"})
     assert (d.drain_q8, d.drain_casts, d.fit_paths) == (0, 4, 0)
     assert c.film_budget_bytes == 4 << 30 and c.public_refill_idle == 16
@@ -186,7 +186,7 @@ def test_config_defaults_and_env_overrides():
                                          ("queue_cache", 3), ("drain_q8", 65536), ("drain_grid_q8", 4097),
                                          ("drain_casts", 65), ("fit_streams", 0), ("fit_streams", 5),
                                          ("fit_paths", (1 << 31) + 1), ("lockstep_first", 4), ("fit_chunks", 2),
-                                         ("drain_refill_idle", 0), ("drain_refill_idle", 65)])
+                                         ("drain_refill_idle", 65)])
 def test_config_validation_without_gpu(field, value):
     c = sptamd.default_config()
     setattr(c, field, value)
