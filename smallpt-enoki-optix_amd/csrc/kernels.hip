@@ -104,6 +104,11 @@ __device__ __forceinline__ void stq2(float2* p, float2 x) {
 #ifndef SPT_DRAIN_WAVES_NT
 #define SPT_DRAIN_WAVES_NT 6
 #endif
+// lane loops (render_fused_kernel): continued and refilled lanes set up their
+// new rays in one tr.init after the refill instead of one each
+#ifndef SPT_MERGED_INIT
+#define SPT_MERGED_INIT 1
+#endif
 
 // Diagnostic build only (make BUILD=build_wlog EXTRA=-DSPT_WAVE_LOG=1,
 // tools/wave_log.py): every wave of a lane-loop launch (fused kernel, drain)
@@ -122,6 +127,13 @@ struct WaveRec {
 constexpr uint32_t kWaveLogMax = 1u << 18;
 __device__ uint32_t g_wlog_n;
 __device__ WaveRec g_wlog[kWaveLogMax];
+// ... and, summed over every wave of the lane-loop launches, where a wave's
+// time goes (shader clock, s_memtime): [0] cycles in trace steps, [1] cycles
+// in shade + refill passes, [2] trace steps, [3] passes, [4] busy lanes summed
+// over trace steps, [5] lanes shaded, [6] lanes refilled, [7] cycles in the
+// refill part of the passes
+constexpr uint32_t kPhaseWords = 8;
+__device__ unsigned long long g_phase[kPhaseWords];
 #endif
 
 // ------------------------------------------------------------- traversal
@@ -1484,6 +1496,7 @@ __attribute__((amdgpu_waves_per_eu(kDrain && kMode == kModeUnit ? (kNt ? SPT_DRA
                                    : kDrain ? SPT_DRAIN_WAVES_RGB : SPT_FUSED_WAVES, 8)))
 void render_fused_kernel(FusedArgs a) {
     constexpr bool kEmit = kMode == kModeEmit;
+    constexpr bool kMergedInit = SPT_MERGED_INIT != 0;
 #if SPT_WAVE_LOG
     const unsigned long long wl_t0 = (unsigned long long)wall_clock64();
 #endif
@@ -1542,11 +1555,20 @@ void render_fused_kernel(FusedArgs a) {
     uint32_t pool = wave_id * share, pool_end = pool + share;
     bool drained = false;
     uint32_t xcd = wave_uniform(blockIdx.x & 7u), xcd_tries = 0;
+#if SPT_WAVE_LOG
+    unsigned long long ph[kPhaseWords] = {};
+#endif
     while (true) {
         if ((uint32_t)__popcll(__ballot(!busy)) >= a.refill_idle) {
+#if SPT_WAVE_LOG
+            const unsigned long long ph_t0 = __builtin_readcyclecounter();
+            ph[3]++;
+            ph[5] += (uint32_t)__popcll(__ballot(pending));
+#endif
             // ---- shade every pending lane (shade_kernel, main.cpp:404-425)
             casts += (uint32_t)__popcll(__ballot(pending));
             bool cont = false;
+            bool need_init = false;  // kMergedInit: a new ray in tr.o / dir to set up after the refill
             if (pending) {
                 pending = false;
                 bool term = true;
@@ -1623,7 +1645,12 @@ void render_fused_kernel(FusedArgs a) {
                                 park[0] = make_float4(thr, thg, thb, lr);
                                 park[1] = make_float4(lg, lb, 0.0f, 0.0f);
                             }
-                            tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 2 >= a.max_depth && !kEmit, L);
+                            if constexpr (kMergedInit) {
+                                tr.o = hp;  // traced from here: set up below with the refilled lanes
+                                need_init = true;
+                            } else {
+                                tr.init(a.sc, hp, dir, kRayTmin, kRayTmax, depth + 2 >= a.max_depth && !kEmit, L);
+                            }
                             busy = true;
                             cont = true;
                         }
@@ -1642,6 +1669,9 @@ void render_fused_kernel(FusedArgs a) {
                 }
             }
             conts += (uint32_t)__popcll(__ballot(cont));
+#if SPT_WAVE_LOG
+            const unsigned long long ph_t2 = __builtin_readcyclecounter();
+#endif
             // ---- new camera paths in free lanes (refill_kernel)
             uint64_t idle = __ballot(!busy && !pending);
             while (idle && !(drained && pool == pool_end)) {
@@ -1702,11 +1732,17 @@ void render_fused_kernel(FusedArgs a) {
                         park[0] = make_float4(thr, thg, thb, lr);
                         park[1] = make_float4(lg, lb, 0.0f, 0.0f);
                     }
-                    tr.init(a.sc, v3(q1.x, q1.y, q1.z), dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit, L);
                     busy = true;
-                    if (tr.finished()) {  // empty scene: a miss
-                        busy = false;
-                        pending = true;
+                    if constexpr (kMergedInit) {
+                        tr.o = v3(q1.x, q1.y, q1.z);
+                        need_init = true;
+                    } else {
+                        tr.init(a.sc, v3(q1.x, q1.y, q1.z), dir, kRayTmin, kRayTmax, depth + 1 >= a.max_depth && !kEmit,
+                                L);
+                        if (tr.finished()) {  // empty scene: a miss
+                            busy = false;
+                            pending = true;
+                        }
                     }
                 } else if (!kDrain && !busy && !pending && rank < take) {
                     uint32_t sample;
@@ -1724,23 +1760,55 @@ void render_fused_kernel(FusedArgs a) {
                         park[0] = make_float4(thr, thg, thb, lr);
                         park[1] = make_float4(lg, lb, 0.0f, 0.0f);
                     }
-                    tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit, L);
                     busy = true;
-                    if (tr.finished()) {  // empty scene: a miss
-                        busy = false;
-                        pending = true;
+                    if constexpr (kMergedInit) {
+                        tr.o = o;
+                        need_init = true;
+                    } else {
+                        tr.init(a.sc, o, dir, kRayTmin, kRayTmax, a.max_depth <= 1 && !kEmit, L);
+                        if (tr.finished()) {  // empty scene: a miss
+                            busy = false;
+                            pending = true;
+                        }
                     }
                 }
                 if (!kDrain) starts += take;
                 pool += take;
+#if SPT_WAVE_LOG
+                ph[6] += take;
+#endif
                 idle = __ballot(!busy && !pending);
             }
+            if (kMergedInit && need_init) {
+                // one ray set-up for the continued and the refilled lanes (one
+                // copy of the code instead of two); the last cast of a path is
+                // an any-hit query (unit mode)
+                tr.init(a.sc, tr.o, dir, kRayTmin, kRayTmax,
+                        (meta & ((1u << kMetaDepthBits) - 1u)) + 1u >= a.max_depth && !kEmit, L);
+                if (tr.finished()) {  // empty scene: a miss
+                    busy = false;
+                    pending = true;
+                }
+            }
+#if SPT_WAVE_LOG
+            const unsigned long long ph_t3 = __builtin_readcyclecounter();
+            ph[1] += ph_t3 - ph_t0;
+            ph[7] += ph_t3 - ph_t2;
+#endif
         }
         if (!__ballot(busy || pending)) break;
+#if SPT_WAVE_LOG
+        const unsigned long long ph_t1 = __builtin_readcyclecounter();
+        ph[2]++;
+        ph[4] += (uint32_t)__popcll(__ballot(busy));
+#endif
         if (busy && tr.step(a.sc, L, st)) {
             busy = false;
             pending = true;
         }
+#if SPT_WAVE_LOG
+        ph[0] += __builtin_readcyclecounter() - ph_t1;
+#endif
     }
 #if SPT_WAVE_LOG
     if ((threadIdx.x & 63u) == 0) {
@@ -1757,6 +1825,8 @@ void render_fused_kernel(FusedArgs a) {
             r.drain = kDrain ? 1u : 0u;
             g_wlog[i] = r;
         }
+        for (uint32_t k = 0; k < kPhaseWords; k++)
+            if (ph[k]) atomicAdd(&g_phase[k], ph[k]);
     }
 #endif
     // the drain: a queued path's first cast here was counted with the queue
@@ -2287,5 +2357,17 @@ extern "C" long long spt_debug_wave_log(void* out, unsigned long long max, int r
         if (hipMemcpyToSymbol(HIP_SYMBOL(spt::g_wlog_n), &z, sizeof(z)) != hipSuccess) return -1;
     }
     return (long long)n;
+}
+
+// Diagnostic build only: the kPhaseWords phase counters (g_phase above) into
+// `out` (8 unsigned 64-bit words), zeroed after when `reset`.
+extern "C" int spt_debug_phase_log(unsigned long long* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(spt::g_phase), sizeof(spt::g_phase)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned long long z[spt::kPhaseWords] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(spt::g_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
 }
 #endif
