@@ -1265,8 +1265,7 @@ __device__ __forceinline__ void shade_block(const ShadeArgs& a, bool valid, cons
                 }
                 o = v3(q1.x, q1.y, q1.z);
                 d = v3(q2.x, q2.y, q2.z);
-                const uint32_t lx = pix % a.W, ly = pix / a.W;
-                gpix = tile_global_row(ly, a.tile_index, a.tile_count, a.rows_per_group) * a.W + lx;
+                gpix = tile_global_pixel(pix, a.W, a.tile_index, a.tile_count, a.rows_per_group);
             }
             if (kMode == kModeUnit) {
                 term = !bounce;  // albedo 1: the throughput stays 1, roulette never fires
@@ -1599,7 +1598,7 @@ void render_fused_kernel(FusedArgs a) {
                     if (depth + 1 < a.max_depth) {
                         // the global pixel (main.cpp:379-382), for the roulette draw and the PCG32 stream
                         const uint32_t gpix =
-                            tile_global_row(pix / a.W, a.tile_index, a.tile_count, a.rows_per_group) * a.W + pix % a.W;
+                            tile_global_pixel(pix, a.W, a.tile_index, a.tile_count, a.rows_per_group);
                         if (kMode != kModeUnit) {
                             const V3 rf = reflectance(a.sc, mat, (uint32_t)slot, hh.u, hh.v);  // main.cpp:418
                             thr = thr * rf.x;                        // main.cpp:422

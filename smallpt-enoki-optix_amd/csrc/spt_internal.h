@@ -442,6 +442,13 @@ SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_
     uint32_t g = local_row / rows_per_group;
     return (g * tile_count + tile_index) * rows_per_group + local_row % rows_per_group;
 }
+// Tile pixel -> global pixel (main.cpp:379-382's index); a whole image (one
+// tile) is its own tile, so the two divisions are skipped (a wave-uniform test)
+SPT_HD uint32_t tile_global_pixel(uint32_t pix, uint32_t W, uint32_t tile_index, uint32_t tile_count,
+                                  uint32_t rows_per_group) {
+    if (tile_count == 1u) return pix;
+    return tile_global_row(pix / W, tile_index, tile_count, rows_per_group) * W + pix % W;
+}
 
 // Tile pixel of the q-th camera path of a sample (q in [0, P), P = W * H):
 // row bands of B rows, each cut into B-wide blocks taken in order, q running
