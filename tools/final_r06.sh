@@ -4,8 +4,10 @@
 # faults or aborts).  Output: gpurun_out/r06_final/ (copied to profiles/).
 #   bash tools/final_r06.sh a    suite, smoke, default bench (+ CPU baseline, parity),
 #                                single-render bench, kernel trace of the default bench
-#   bash tools/final_r06.sh b    configs 0, 2, 3, 4 (+ CPU baselines), PMC passes of the
-#                                config-2 / config-3 drains, tile projection x3
+#   bash tools/final_r06.sh b    configs 0, 2, 3, 4 (+ CPU baselines), tile projection x3
+#                                (PMC=1: also the PMC passes of the config-2 / config-3 drains;
+#                                the final build's passes of every config ran on their own:
+#                                profiles/r06_pmc2/, r06_pmc3/)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -37,8 +39,10 @@ case "${1:-a}" in
     ;;
   b)
     for c in 0 2 3 4; do step bench$c 500 python bench.py --config $c --steps 2 --warmup 1; done
-    step pmcd2 600 env CONFIG=2 KERNEL=drain bash tools/pmc_isect.sh $O/pmc
-    step pmcd3 600 env CONFIG=3 KERNEL=drain bash tools/pmc_isect.sh $O/pmc
+    if [ "${PMC:-0}" = 1 ]; then
+      step pmcd2 600 env CONFIG=2 KERNEL=drain bash tools/pmc_isect.sh $O/pmc
+      step pmcd3 600 env CONFIG=3 KERNEL=drain bash tools/pmc_isect.sh $O/pmc
+    fi
     for r in 1 2 3; do step tiles$r 300 python tools/tile_sim.py --tiles 1 2 4 8 --steps 8; done
     ;;
 esac
