@@ -458,6 +458,14 @@ Camera make_camera(const spt_render_params& p) {
     cam.ratio = (float)p.width / (float)p.height;
     cam.fw = (float)p.width;
     cam.fh = (float)p.height;
+    // exact reciprocals of power-of-two sizes (camera_sample_dir), else 0
+    cam.inv_fw = p.width && (p.width & (p.width - 1u)) == 0u ? 1.0f / cam.fw : 0.0f;
+    cam.inv_fh = p.height && (p.height & (p.height - 1u)) == 0u ? 1.0f / cam.fh : 0.0f;
+    {
+        volatile float fz = cam.dist_lens_to_film;  // the device's operation order, no folding
+        volatile float num = cam.focal_dist * fz;
+        cam.focal_z = num / fz;
+    }
     return cam;
 }
 

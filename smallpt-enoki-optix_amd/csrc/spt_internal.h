@@ -439,6 +439,7 @@ struct HitInfoArgs {
 // Tile-local row -> global row for interleaved row groups.
 SPT_HD uint32_t tile_global_row(uint32_t local_row, uint32_t tile_index, uint32_t tile_count,
                                 uint32_t rows_per_group) {
+    if (tile_count == 1u) return local_row;  // one tile: the identity below, without its divisions
     uint32_t g = local_row / rows_per_group;
     return (g * tile_count + tile_index) * rows_per_group + local_row % rows_per_group;
 }
@@ -466,7 +467,7 @@ SPT_HD uint32_t tile_global_pixel(uint32_t pix, uint32_t W, uint32_t tile_index,
 // both.  Both cover every (sample, pixel) of the chunk once.
 SPT_HD void work_item(uint32_t local, uint32_t s0, uint32_t ns, uint32_t P, bool pm, uint32_t& s, uint32_t& q) {
     const uint32_t d = pm ? ns : P;
-    const uint32_t a = local / d, b = local - a * d;
+    const uint32_t a = udiv(local, d), b = local - a * d;
     s = s0 + (pm ? b : a);
     q = pm ? a : b;
 }
@@ -485,7 +486,7 @@ SPT_HD float* film_rgb(float* sfilm, uint32_t sl, uint32_t pix, uint32_t P, uint
 }
 
 SPT_HD void work_pixel(uint32_t q, uint32_t W, uint32_t P, uint32_t B, uint32_t& lx, uint32_t& ly) {
-    if (B <= 1) { lx = q % W; ly = q / W; return; }
+    if (B <= 1) { ly = udiv(q, W); lx = q - ly * W; return; }
     const uint32_t H = P / W;
     const uint32_t band = q / (B * W);
     const uint32_t off = q - band * B * W;

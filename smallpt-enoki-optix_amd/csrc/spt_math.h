@@ -23,6 +23,12 @@ constexpr float kBoxPad = 1.000001f;  // conservative slab exit (Ize 2013 + marg
 
 SPT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 SPT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+// n / d for a wave-uniform d: a shift when d is a power of two (image sizes,
+// sample counts), the divide otherwise
+SPT_HD uint32_t udiv(uint32_t n, uint32_t d) {
+    if ((d & (d - 1u)) == 0u) return n >> (uint32_t)__builtin_ctz(d);
+    return n / d;
+}
 
 // ------------------------------------------------------------------ PCG32
 // Enoki random.h (external): next_uint32 / next_float32; seeded at
@@ -165,6 +171,10 @@ struct Camera {
     Frame frame;
     float lens_radius, focal_dist, dist_lens_to_film, ratio, film_y;
     float fw, fh;  // image resolution as float
+    // 1 / fw and 1 / fh when fw, fh are powers of two, else 0: then x / fw and
+    // x * (1 / fw) are the same correctly rounded value, bit for bit
+    float inv_fw, inv_fh;
+    float focal_z;  // (focal_dist * fz) / fz of sample_dir (pinhole.h:47), a per-camera constant
 };
 
 // pinhole.h:27-32
@@ -179,12 +189,15 @@ SPT_HD V3 camera_sample_pos(const Camera& c, float xi_x, float xi_y) {
 // pinhole.h:34-56
 SPT_HD V3 camera_sample_dir(const Camera& c, uint32_t px, uint32_t py, V3 pos, float xi_x, float xi_y) {
     V3 lens = to_local(c.frame, pos - c.origin);
-    float ndc_x = ((float)px + xi_x) / c.fw;
-    float ndc_y = ((float)py + xi_y) / c.fh;
+    float ndc_x, ndc_y;
+    if (c.inv_fw != 0.0f) ndc_x = ((float)px + xi_x) * c.inv_fw;
+    else ndc_x = ((float)px + xi_x) / c.fw;
+    if (c.inv_fh != 0.0f) ndc_y = ((float)py + xi_y) * c.inv_fh;
+    else ndc_y = ((float)py + xi_y) / c.fh;
     float fx = (0.5f - ndc_x) * (c.ratio * c.film_y);
     float fy = (0.5f - ndc_y) * c.film_y;
     float fz = c.dist_lens_to_film;
-    V3 focal = {(c.focal_dist * fx) / fz, (c.focal_dist * fy) / fz, (c.focal_dist * fz) / fz};
+    V3 focal = {(c.focal_dist * fx) / fz, (c.focal_dist * fy) / fz, c.focal_z};
     return to_world(c.frame, normalize(focal - lens));
 }
 

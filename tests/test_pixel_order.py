@@ -13,6 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "smallpt-enoki-optix_amd", "csrc", "spt_internal.h")
+MATH_SRC = os.path.join(ROOT, "smallpt-enoki-optix_amd", "csrc", "spt_math.h")
 
 MAIN = r"""
 #include <cstdio>
@@ -56,10 +57,13 @@ def checker(tmp_path_factory):
     src = open(SRC).read()
     m = re.search(r"^SPT_HD void work_pixel\(.*?^}\n", src, re.S | re.M)
     assert m, "work_pixel not found in spt_internal.h"
+    # its division helper (a shift for power-of-two widths), from spt_math.h
+    u = re.search(r"^SPT_HD uint32_t udiv\(.*?^}\n", open(MATH_SRC).read(), re.S | re.M)
+    assert u, "udiv not found in spt_math.h"
     d = tmp_path_factory.mktemp("pixorder")
     cpp = d / "pixorder.cpp"
     cpp.write_text("#include <cstdint>\n#include <cstdlib>\n#include <vector>\n#define SPT_HD static inline\n"
-                   + m.group(0) + MAIN)
+                   + u.group(0) + m.group(0) + MAIN)
     exe = d / "pixorder"
     subprocess.run([gxx, "-O2", "-std=c++17", "-o", str(exe), str(cpp)], check=True)
     return exe
