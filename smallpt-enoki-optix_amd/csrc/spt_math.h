@@ -157,7 +157,9 @@ SPT_HD void disk_from_square(float xi_x, float xi_y, float& ox, float& oy) {
     float ax2 = ax * ax, ay2 = ay * ay;
     bool cond = ax2 > ay2;
     float r = cond ? ax : ay;
-    float phi = cond ? (kPi / 4.0f) * (ay / ax) : (kPi / 2.0f) - (kPi / 4.0f) * (ax / ay);
+    // one divide for either branch (the lanes of a wave take both)
+    const float q = (cond ? ay : ax) / (cond ? ax : ay);
+    float phi = cond ? (kPi / 4.0f) * q : (kPi / 2.0f) - (kPi / 4.0f) * q;
     float s, c;
     sincos_cephes(phi, s, c);
     ox = r * c;
