@@ -594,7 +594,7 @@ def main():
                            "wavefront_casts_per_step": round((agg["ray_casts"] - agg["drained_casts"]) / args.steps),
                            "drain_launches_per_step": round(agg["drain_launches"] / args.steps, 2),
                            "refill_idle": st.get("drain_refill_idle"),
-                           "refill_idle_rule": "auto (drain_refill_idle 0): 56 for scenes of <= 1024 triangles, "
+                           "refill_idle_rule": "auto (drain_refill_idle 0): 56 for scenes with analytic spheres, "
                                                "40 when the queue is streamed, else 24 (DESIGN.md §4)"
                                                if scene.backend.config["drain_refill_idle"] == 0 else "set"},
                        "hw_queues": {"in_effect": os.environ.get("GPU_MAX_HW_QUEUES", "unset (HIP default 4)"),

@@ -347,11 +347,11 @@ typedef struct spt_config {
                                        halves the fit and retries.  The image does not depend on
                                        it                                                      */
     uint32_t drain_refill_idle;     /* the drain's lane loop refills (and shades) once this many of a
-                                       wave's lanes are idle.  0 = AUTO: 56 for scenes of at most
-                                       1024 triangles (a trace step is cheap next to a refill:
-                                       config 2 +20 % over 24), 40 when the queue is streamed
-                                       (queue_cache; config 4 +3 %), else 24 (config 1 +1.8 %
-                                       over 32).  The fused kernel keeps fused_refill_idle.
+                                       wave's lanes are idle.  0 = AUTO: 56 for scenes with analytic
+                                       spheres (tested in the shade: a pass costs several
+                                       trace steps; config 2 +20 % over 24), 40 when the queue
+                                       is streamed (queue_cache; config 4 +3 %), else 24
+                                       (config 1 +1.8 % over 32).  The fused kernel keeps fused_refill_idle.
                                        The image does not depend on it   [0..64] */
 } spt_config;
 

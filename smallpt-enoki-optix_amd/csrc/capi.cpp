@@ -2103,15 +2103,15 @@ retry_fit:
     // The drain's refill threshold (spt_config.drain_refill_idle).  AUTO: a
     // wave refills and shades once per batch of free lanes, at a cost that
     // does not depend on how many lanes take part, while a trace step costs
-    // in proportion to how long its busiest lane traverses.  A scene of a few
-    // triangles (smallpt's walls: the spheres are tested in the shade) traces
-    // in a step or two, so batching more lanes pays (config 2: 56 +20 % over
-    // 24); a scene beyond the Infinity Cache (config 4) +3 % at 40; the
-    // cache-resident mitsuba mesh -2 % at 32 (configs 1, 3), while the
-    // tessellated Cornell spheres (75k triangles) gain 1-6 % at 40: the rule
-    // keys on what the benchmarks separate (profiles/r06_exp/refill_idle/).
+    // in proportion to how long its busiest lane traverses.  With analytic
+    // spheres the shade tests them and runs smallpt's mirror / glass, so a
+    // pass costs several trace steps and batching more lanes pays (config 2:
+    // 56 +20 % over 24); a scene beyond the Infinity Cache (config 4) +3 % at
+    // 40; triangle scenes 24 (configs 1, 3, and the mitsuba mesh from 200 to
+    // 231k triangles: 56 costs 13-17 %), though closed ones (the tessellated
+    // Cornell spheres) gain 1-3 % at 40 (profiles/r06_exp/refill_idle/).
     const uint32_t drain_idle = cfg.drain_refill_idle ? cfg.drain_refill_idle
-                                : sc->ntri <= kTraceLightTris ? kDrainIdleTraceLight
+                                : sc->nsph > 0 ? kDrainIdleSpheres
                                 : queue_nt ? kDrainIdleStream : kDrainIdleCached;
     if (cfg.work_order == SPT_WORK_AUTO && wave_pm && !p.wavefront_paths && cfg.wavefront_paths == kDefaultWavefrontPaths)
         C = kPixelMajorWavefrontPaths;

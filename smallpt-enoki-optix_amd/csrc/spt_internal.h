@@ -66,12 +66,10 @@ constexpr uint64_t kDefaultFitPaths = 1ull << 28;
 // sub-wavefront's last work item started, whatever its queue holds
 constexpr uint32_t kDefaultDrainCasts = 1;
 // spt_config.drain_refill_idle AUTO (0): free lanes a drain wave waits for
-// before it refills and shades — scenes of at most kTraceLightTris triangles
-// (a BVH of a few hundred leaves: a trace step is cheap next to a refill;
-// config 2's smallpt walls are 640), scenes whose queue is streamed (beyond
-// the Infinity Cache), the rest
-constexpr uint64_t kTraceLightTris = 1024;
-constexpr uint32_t kDrainIdleTraceLight = 56;
+// before it refills and shades — scenes with analytic spheres (tested in the
+// shade, with smallpt's mirror / glass: the pass costs several trace steps),
+// scenes whose queue is streamed (beyond the Infinity Cache), the rest
+constexpr uint32_t kDrainIdleSpheres = 56;
 constexpr uint32_t kDrainIdleStream = 40;
 constexpr uint32_t kDrainIdleCached = 24;
 

@@ -318,8 +318,8 @@ def test_xcd_pools_bitexact(mesh, mode, lockstep, w, h, monkeypatch):
 @pytest.mark.parametrize("idle", [0, 1, 40, 64])
 def test_drain_refill_idle_bitexact(mesh, mode, idle, monkeypatch):
     """spt_config.drain_refill_idle: the drain's refill threshold (AUTO: 24 for
-    this cache-resident mesh of more than 1024 triangles, 40 with the queue
-    streamed) only reorders the drain's work — same bits, same casts."""
+    this cache-resident mesh, 40 with the queue streamed, 56 with analytic
+    spheres) only reorders the drain's work — same bits, same casts."""
     for k in [k for k in list(__import__("os").environ) if k.startswith("SPT_")]:
         monkeypatch.delenv(k)
     mat = materials(mesh, mode)
@@ -333,5 +333,5 @@ def test_drain_refill_idle_bitexact(mesh, mode, idle, monkeypatch):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(film.cpu().numpy(), ref)
         assert st["ray_casts"] == casts and st["drained_paths"] > 0
-        auto = 40 if cache == sptamd._lib.SPT_QUEUE_CACHE_STREAM else 24
+        auto = 56 if "spheres" in mat else 40 if cache == sptamd._lib.SPT_QUEUE_CACHE_STREAM else 24
         assert st["drain_refill_idle"] == (idle or auto)

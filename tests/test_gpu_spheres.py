@@ -58,7 +58,7 @@ def test_smallpt_scene_bitexact(mesh, pipeline, rr):
 
 @pytest.mark.parametrize("idle", [0, 1, 24, 64])
 def test_smallpt_drain_refill_idle(mesh, idle, monkeypatch):
-    """spt_config.drain_refill_idle on smallpt's scene (a few wall triangles:
+    """spt_config.drain_refill_idle on smallpt's scene (analytic spheres:
     AUTO picks 56): when a drain wave refills changes only the
     order of the work, not the bits."""
     monkeypatch.delenv("SPT_DRAIN_IDLE", raising=False)
